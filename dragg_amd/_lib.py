@@ -1,0 +1,117 @@
+"""ctypes binding of the C ABI in include/dragg_mi355x.h (libdragg_mi355x.so).
+
+The library is built in-tree (dragg_amd/libdragg_mi355x.so, see dragg_amd/build.py).
+There is deliberately no CPU fallback: if the library or a GPU is missing, every
+entry point raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdragg_mi355x.so")
+
+ABI_VERSION = 1
+
+# enums (mirror include/dragg_mi355x.h)
+BASE, PV_ONLY, BATTERY_ONLY, PV_BATTERY = 0, 1, 2, 3
+TYPE_CODE = {"base": BASE, "pv_only": PV_ONLY, "battery_only": BATTERY_ONLY, "pv_battery": PV_BATTERY}
+
+PARAMS = ["R", "C", "PC", "PH", "RW", "PW", "CW", "V", "TMIN", "TMAX", "TWMIN", "TWMAX", "TINIT",
+          "TWINIT", "BRATE", "EMIN", "EMAX", "ETAC", "ETAD", "EINIT", "PVAREA", "PVEFF"]
+NPARAM = len(PARAMS)
+P = {k: i for i, k in enumerate(PARAMS)}
+
+FC_KEYS = ["p_grid_opt", "forecast_p_grid_opt", "p_load_opt", "temp_in_ev_opt", "temp_wh_ev_opt",
+           "hvac_cool_on_opt", "hvac_heat_on_opt", "wh_heat_on_opt", "cost_opt", "waterdraws",
+           "p_pv_opt", "u_pv_curt_opt", "p_batt_ch", "p_batt_disch", "e_batt_opt"]
+NFC = len(FC_KEYS)
+VAL_KEYS = FC_KEYS + ["temp_in_opt", "temp_wh_opt", "correct_solve", "solve_counter"]
+NVAL = len(VAL_KEYS)
+K = {k: i for i, k in enumerate(VAL_KEYS)}
+
+ST_OPTIMAL, ST_INFEASIBLE, ST_INFEASIBLE_CERT, ST_MAX_ITER, ST_ROUND_FAIL, ST_ERR_PARSE, ST_ERR_MISSING = range(7)
+STATUS_NAMES = ["optimal", "infeasible", "infeasible_cert", "max_iter", "round_fail", "err_parse",
+                "err_missing"]
+
+INT_ROUND, INT_RELAX = 0, 1
+
+c_dp = ctypes.c_void_p  # device pointers are passed as raw integers
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [("n_homes", ctypes.c_int32), ("horizon", ctypes.c_int32), ("sub_steps", ctypes.c_int32),
+                ("dt", ctypes.c_int32), ("n_draw_hours", ctypes.c_int32), ("n_env", ctypes.c_int32),
+                ("n_rp", ctypes.c_int32), ("int_mode", ctypes.c_int32), ("max_iter", ctypes.c_int32),
+                ("check_every", ctypes.c_int32), ("discount", ctypes.c_double)]
+
+
+class Problem(ctypes.Structure):
+    _fields_ = [("params", c_dp), ("home_type", c_dp), ("draw_hourly", c_dp), ("oat", c_dp), ("ghi", c_dp),
+                ("tou", c_dp), ("reward_price", c_dp), ("start_index", ctypes.c_int32),
+                ("_pad", ctypes.c_int32), ("seed", ctypes.c_uint64)]
+
+
+class Hash(ctypes.Structure):
+    _fields_ = [("vals", c_dp), ("fc", c_dp)]
+
+
+class Out(ctypes.Structure):
+    _fields_ = [("status", c_dp), ("iters", c_dp), ("obj", c_dp), ("relax_obj", c_dp), ("hist", c_dp)]
+
+
+class Explicit(ctypes.Structure):
+    _fields_ = [("t", c_dp), ("T0", c_dp), ("Tw0", c_dp), ("E0", c_dp), ("counter", c_dp), ("winter", c_dp),
+                ("draw", c_dp), ("oat", c_dp), ("ghi", c_dp), ("price", c_dp)]
+
+
+EXPORTS = ["dragg_mpc_abi_version", "dragg_mpc_strerror", "dragg_mpc_lds_bytes", "dragg_mpc_step",
+           "dragg_mpc_solve_explicit", "dragg_mpc_aggregate", "dragg_mpc_season_noise"]
+
+_LIB = None
+
+
+class DraggError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load the HIP library (raises if it was not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise DraggError(f"{path} not found: build it with `python -m dragg_amd.build` "
+                         "(there is no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    lib.dragg_mpc_abi_version.restype = ctypes.c_int
+    lib.dragg_mpc_strerror.restype = ctypes.c_char_p
+    lib.dragg_mpc_strerror.argtypes = [ctypes.c_int]
+    lib.dragg_mpc_lds_bytes.argtypes = [ctypes.POINTER(Dims)]
+    lib.dragg_mpc_step.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Problem), ctypes.POINTER(Hash),
+                                   ctypes.POINTER(Out), ctypes.c_int32, c_dp, c_dp]
+    lib.dragg_mpc_solve_explicit.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Problem),
+                                             ctypes.POINTER(Explicit), ctypes.POINTER(Hash),
+                                             ctypes.POINTER(Out), c_dp]
+    lib.dragg_mpc_aggregate.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Hash), c_dp, c_dp]
+    lib.dragg_mpc_season_noise.argtypes = [ctypes.POINTER(Dims), ctypes.c_uint64, ctypes.c_int32, c_dp, c_dp]
+    if lib.dragg_mpc_abi_version() != ABI_VERSION:
+        raise DraggError("ABI version mismatch between dragg_amd and libdragg_mi355x.so")
+    _LIB = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        raise DraggError(f"dragg_mpc error {rc}: {load().dragg_mpc_strerror(rc).decode()}")
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)

@@ -1,0 +1,1061 @@
+// mpc_kernel.hip -- batched per-home HEMS MPC for MI355X (gfx950, CDNA4).
+//
+// One 64-lane workgroup (one wavefront) owns one home for one timestep.  The home's
+// MILP from dragg/mpc_calc.py:291-446 is rebuilt on device in a stage-ordered chain
+// form (8 variable slots and 3 dynamics rows per stage), the LP relaxation is solved
+// by an OSQP-style ADMM whose block-tridiagonal KKT factor (8x8 blocks, lane (i,j) of
+// the wave owns entry (i,j)) lives in LDS, and every `check_every` iterations an exact
+// basis polish recovers the vertex and certifies it (primal feasibility + reduced-cost
+// signs).  The integer duty cycles are then rounded feasibly, and the reference's
+// result extraction / fallback thermostat (mpc_calc.py:476-596) writes the per-home
+// hash arrays in place.  See DESIGN.md for the formulation and roofline.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/dragg_mi355x.h"
+
+#define DEV static __device__ __forceinline__
+
+namespace {
+
+constexpr int NS = 8;        // variable slots per stage
+constexpr int NR = 3;        // dynamics rows per stage
+constexpr int RS = 4;        // row stride per stage in LDS
+constexpr int WAVE = 64;
+enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
+
+constexpr double SIGMA = 1e-6;
+constexpr double ALPHA = 1.6;
+constexpr double RHO0 = 0.1;
+constexpr double RHO_EQ = 1e3;      // equality rows get RHO_EQ * rho (OSQP convention)
+constexpr double TAP = 15.0;        // mpc_calc.py:181
+constexpr double EPS_PINF = 1e-5;
+constexpr double TOL_P = 1e-9;
+constexpr double TOL_D = 1e-9;
+
+// --------------------------------------------------------------------------------------
+// LDS carve
+// --------------------------------------------------------------------------------------
+struct Lds {
+    double *Lf, *Df;                   // [H][64] sub-diagonal factor blocks, inverse pivots
+    double *al, *be, *beq;             // [H][3][8], [H][3][8], [H][4]
+    double *x, *zb, *yb, *lo, *hi, *q; // [8H]
+    double *r, *t1, *t2;               // [8H] rhs / solve temporaries
+    double *ybp;                       // [8H] previous box duals (certificate)
+    double *yeq, *zeq, *yeqp, *lam;    // [4H], [4H], [4H], [4(H+1)]
+    double *draw, *oat, *ghi, *price;  // [H+1], [H+1], [H+1], [H+1]
+    double *sc;                        // [32] scalars
+    int *at, *basic;                   // [8H], [4H]
+};
+
+__host__ __device__ inline int lds_doubles(int H) {
+    return 64 * H * 2 + 24 * H * 2 + 4 * H + 8 * H * 10 + 4 * H * 3 + 4 * (H + 1) + 4 * (H + 1) + 32 +
+           (8 * H + 4 * H + 1) / 2 + 2;
+}
+
+DEV Lds carve(double* s, int H) {
+    Lds L;
+    L.Lf = s; s += 64 * H;
+    L.Df = s; s += 64 * H;
+    L.al = s; s += 24 * H;
+    L.be = s; s += 24 * H;
+    L.beq = s; s += 4 * H;
+    L.x = s; s += 8 * H;
+    L.zb = s; s += 8 * H;
+    L.yb = s; s += 8 * H;
+    L.lo = s; s += 8 * H;
+    L.hi = s; s += 8 * H;
+    L.q = s; s += 8 * H;
+    L.r = s; s += 8 * H;
+    L.t1 = s; s += 8 * H;
+    L.t2 = s; s += 8 * H;
+    L.ybp = s; s += 8 * H;
+    L.yeq = s; s += 4 * H;
+    L.zeq = s; s += 4 * H;
+    L.yeqp = s; s += 4 * H;
+    L.lam = s; s += 4 * (H + 1);
+    L.draw = s; s += H + 1;
+    L.oat = s; s += H + 1;
+    L.ghi = s; s += H + 1;
+    L.price = s; s += H + 1;
+    L.sc = s; s += 32;
+    L.at = reinterpret_cast<int*>(s);
+    L.basic = L.at + 8 * H;
+    return L;
+}
+
+// --------------------------------------------------------------------------------------
+// wave helpers
+// --------------------------------------------------------------------------------------
+DEV double sum8(double v) {           // sum over the 8 lanes of a group (lane bits 0..2)
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    return v;
+}
+DEV double wave_max(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+DEV double wave_sum(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+DEV bool wave_any(bool p) { return __any(p); }
+
+// --------------------------------------------------------------------------------------
+// keyed season noise: Philox4x32-10 + Box-Muller (replaces the worker-global
+// np.random.randn of mpc_calc.py:222, which is not reproducible across runs)
+// --------------------------------------------------------------------------------------
+DEV void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+}
+DEV void normal_pair(uint64_t seed, int home, int t, int pair, double* z0, double* z1) {
+    uint32_t c[4] = {(uint32_t)home, (uint32_t)t, (uint32_t)pair, 0u};
+    philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint64_t a = ((uint64_t)(c[0] >> 5) << 26) | (c[1] >> 6);
+    const uint64_t b = ((uint64_t)(c[2] >> 5) << 26) | (c[3] >> 6);
+    const double u1 = ((double)a + 1.0) * 0x1.0p-53;   // (0, 1]
+    const double u2 = (double)b * 0x1.0p-53;           // [0, 1)
+    const double rad = sqrt(-2.0 * log(u1));
+    const double th = 6.283185307179586 * u2;
+    *z0 = rad * cos(th);
+    *z1 = rad * sin(th);
+}
+
+// Python's float(repr(v)[0]) for the fallback's duty parse (mpc_calc.py:537-539).
+// repr uses scientific notation below 1e-4.  Returns -1 where the reference raises.
+DEV double leading_char_value(double v) {
+    if (!(v == v) || isinf(v) || v < 0.0 || signbit(v)) return -1.0;   // 'n', 'i', '-'
+    if (v == 0.0) return 0.0;
+    if (v >= 1e-4) return v < 1.0 ? 0.0 : floor(v / pow(10.0, floor(log10(v))));
+    double e = floor(log10(v));
+    double d = floor(v / pow(10.0, e));
+    if (d >= 10.0) d = 9.0;
+    if (d < 1.0) d = 1.0;
+    return d;
+}
+
+// --------------------------------------------------------------------------------------
+// per-home scalars (registers, identical in every lane)
+// --------------------------------------------------------------------------------------
+struct Home {
+    int H, S, dt, type, nrows;
+    bool batt, pv, winter;
+    double R, C, Pc, Ph, Rw, Pw, Cw, V, Tmin, Tmax, Twmin, Twmax, Tinit, Twinit;
+    double brate, Emin, Emax, etac, etad, Einit, pvA, pvEta;
+    double gamma;
+    // derived
+    double inv_c, inv_w, iR, iRw, aT, g, e, f, Pact;
+    // step inputs
+    int t, counter;
+    double T0, Tw0, E0;
+};
+
+DEV void load_params(Home& h, const double* P, int N, int i) {
+    h.R = P[DRAGG_P_R * N + i];       h.C = P[DRAGG_P_C * N + i];
+    h.Pc = P[DRAGG_P_PC * N + i];     h.Ph = P[DRAGG_P_PH * N + i];
+    h.Rw = P[DRAGG_P_RW * N + i];     h.Pw = P[DRAGG_P_PW * N + i];
+    h.Cw = P[DRAGG_P_CW * N + i];     h.V = P[DRAGG_P_V * N + i];
+    h.Tmin = P[DRAGG_P_TMIN * N + i]; h.Tmax = P[DRAGG_P_TMAX * N + i];
+    h.Twmin = P[DRAGG_P_TWMIN * N + i]; h.Twmax = P[DRAGG_P_TWMAX * N + i];
+    h.Tinit = P[DRAGG_P_TINIT * N + i]; h.Twinit = P[DRAGG_P_TWINIT * N + i];
+    h.brate = P[DRAGG_P_BRATE * N + i]; h.Emin = P[DRAGG_P_EMIN * N + i];
+    h.Emax = P[DRAGG_P_EMAX * N + i];   h.etac = P[DRAGG_P_ETAC * N + i];
+    h.etad = P[DRAGG_P_ETAD * N + i];   h.Einit = P[DRAGG_P_EINIT * N + i];
+    h.pvA = P[DRAGG_P_PVAREA * N + i];  h.pvEta = P[DRAGG_P_PVEFF * N + i];
+}
+
+DEV void derive(Home& h) {
+    h.inv_c = 1.0 / (h.C * h.dt);                 // 1 / (home_c * dt)   mpc_calc.py:317
+    h.inv_w = 1.0 / (h.Cw * h.dt);                // 1 / (wh_c * dt)     mpc_calc.py:332
+    h.iR = 1.0 / h.R;
+    h.iRw = 1.0 / h.Rw;
+    h.aT = 1.0 + (-h.iR * 3600) * h.inv_c;        // coefficient of T_k in T_{k+1}
+    if (h.winter) { h.g = h.Ph * 3600 * h.inv_c;    h.Pact = h.S * h.Ph; }
+    else          { h.g = -(h.Pc * 3600 * h.inv_c); h.Pact = h.S * h.Pc; }
+    h.e = h.iRw * 3600 * h.inv_w;                 // coefficient of T_{k+1} in Tw_{k+1}
+    h.f = h.Pw * 3600 * h.inv_w;                  // coefficient of w_k
+}
+
+DEV bool slot_active(const Home& h, int j) { return j < 4 || (h.batt && j < 7); }
+
+// --------------------------------------------------------------------------------------
+// build the chain LP (add_base/pv/battery_constraints, set_*_p_grid, solve_mpc)
+// --------------------------------------------------------------------------------------
+DEV void build(const Home& h, const Lds& L, int lane) {
+    const int H = h.H;
+    for (int k = lane; k < H; k += WAVE) {
+        double* A = L.al + k * 24;
+        double* B = L.be + k * 24;
+#pragma unroll
+        for (int m = 0; m < 24; ++m) { A[m] = 0.0; B[m] = 0.0; }
+        const double df = L.draw[k + 1] / h.V;
+        const double rem = 1 - df;
+        // indoor air (mpc_calc.py:314-317)
+        A[0 * 8 + S_T] = 1.0; A[0 * 8 + S_U] = -h.g; B[0 * 8 + S_T] = -h.aT;
+        L.beq[k * RS + 0] = L.oat[k + 1] * h.iR * 3600 * h.inv_c;
+        // water heater with draw mixing (mpc_calc.py:330-332)
+        const double ck = rem + (-rem * h.iRw) * 3600 * h.inv_w;
+        const double d15 = df * TAP;
+        A[1 * 8 + S_TW] = 1.0; A[1 * 8 + S_T] = -h.e; A[1 * 8 + S_W] = -h.f; B[1 * 8 + S_TW] = -ck;
+        L.beq[k * RS + 1] = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
+        L.beq[k * RS + 2] = 0.0;
+        L.beq[k * RS + 3] = 0.0;
+        // battery state of charge (mpc_calc.py:363-365)
+        if (h.batt) {
+            A[2 * 8 + S_E] = 1.0; B[2 * 8 + S_E] = -1.0;
+            A[2 * 8 + S_CH] = -h.etac / h.dt;
+            A[2 * 8 + S_DIS] = -(1.0 / h.etad) / h.dt;
+        }
+        // bounds and costs (mpc_calc.py:318-349, 367-372, 441-446)
+        const double w = pow(h.gamma, (double)k) * L.price[k];
+        const int o = k * NS;
+        L.lo[o + S_U] = 0.0;      L.hi[o + S_U] = h.S;      L.q[o + S_U] = w * h.Pact;
+        L.lo[o + S_W] = 0.0;      L.hi[o + S_W] = h.S;      L.q[o + S_W] = w * (h.S * h.Pw);
+        L.lo[o + S_T] = h.Tmin;   L.hi[o + S_T] = h.Tmax;   L.q[o + S_T] = 0.0;
+        L.lo[o + S_TW] = h.Twmin; L.hi[o + S_TW] = h.Twmax; L.q[o + S_TW] = 0.0;
+        if (h.batt) {
+            L.lo[o + S_CH] = 0.0;       L.hi[o + S_CH] = h.brate;  L.q[o + S_CH] = w * h.S;
+            L.lo[o + S_DIS] = -h.brate; L.hi[o + S_DIS] = 0.0;     L.q[o + S_DIS] = w * h.S;
+            L.lo[o + S_E] = h.Emin;     L.hi[o + S_E] = h.Emax;    L.q[o + S_E] = 0.0;
+        } else {
+            L.lo[o + S_CH] = L.hi[o + S_CH] = L.q[o + S_CH] = 0.0;
+            L.lo[o + S_DIS] = L.hi[o + S_DIS] = L.q[o + S_DIS] = 0.0;
+            L.lo[o + S_E] = L.hi[o + S_E] = L.q[o + S_E] = 0.0;
+        }
+        L.lo[o + S_PAD] = L.hi[o + S_PAD] = L.q[o + S_PAD] = 0.0;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        // fold the fixed initial states into stage 0 (mpc_calc.py:313, 329, 366)
+        const double rem1 = 1 - L.draw[1] / h.V;
+        const double c0 = rem1 + (-rem1 * h.iRw) * 3600 * h.inv_w;
+        const double d0 = L.beq[1];
+        L.beq[0] += h.aT * h.T0;
+        L.beq[1] += c0 * h.Tw0;
+        if (h.batt) L.beq[2] += h.E0;
+        // temp_wh (the un-mixed one-step value, mpc_calc.py:336-340) differs from Tw_1 by a
+        // constant, so its bounds become a tightened box on Tw_1.
+        const double Kc = (h.Tw0 + ((-h.Tw0) * h.iRw) * 3600 * h.inv_w) - c0 * h.Tw0 - d0;
+        L.lo[S_TW] = fmax(h.Twmin, h.Twmin - Kc);
+        L.hi[S_TW] = fmin(h.Twmax, h.Twmax - Kc);
+        L.sc[8] = Kc;
+    }
+    __syncthreads();
+}
+
+// Exact forward-interval feasibility of the T and E chains (+ outer test for Tw).
+DEV bool presolve_infeasible(const Home& h, const Lds& L) {
+    if (!(h.Twmin <= h.Tw0 && h.Tw0 <= h.Twmax)) return true;          // temp_wh_ev[0] bounds
+    double Tlo = h.T0, Thi = h.T0, Wlo = h.Tw0, Whi = h.Tw0, Elo = h.E0, Ehi = h.E0;
+    const double gS = h.g * h.S;
+    for (int k = 0; k < h.H; ++k) {
+        const int o = k * NS;
+        const double bk = L.oat[k + 1] * h.iR * 3600 * h.inv_c;
+        double lo = h.aT * Tlo + bk + fmin(0.0, gS), hi = h.aT * Thi + bk + fmax(0.0, gS);
+        Tlo = fmax(lo, L.lo[o + S_T]); Thi = fmin(hi, L.hi[o + S_T]);
+        if (Tlo > Thi + TOL_P * (1 + fabs(Thi))) return true;
+        const double ck = (k == 0) ? 0.0 : -L.be[k * 24 + 1 * 8 + S_TW];
+        const double bw = L.beq[k * RS + 1];           // stage 0 already holds c0*Tw0
+        lo = ck * Wlo + bw + h.e * Tlo; hi = ck * Whi + bw + h.e * Thi + h.f * h.S;
+        Wlo = fmax(lo, L.lo[o + S_TW]); Whi = fmin(hi, L.hi[o + S_TW]);
+        if (Wlo > Whi + TOL_P * (1 + fabs(Whi))) return true;
+        if (h.batt) {
+            lo = Elo - h.brate * (1.0 / h.etad) / h.dt; hi = Ehi + h.brate * h.etac / h.dt;
+            Elo = fmax(lo, h.Emin); Ehi = fmin(hi, h.Emax);
+            if (Elo > Ehi + TOL_P * (1 + fabs(Ehi))) return true;
+        }
+    }
+    return false;
+}
+
+// --------------------------------------------------------------------------------------
+// KKT = sigma I + rho_eq A_eq'A_eq + rho I (box rows): block-tridiagonal, 8x8 blocks,
+// block LDL' with explicit inverse pivots.  lane = 8*i + j owns entry (i, j).
+// --------------------------------------------------------------------------------------
+DEV void factor(const Home& h, const Lds& L, int lane, double rho) {
+    const int i = lane >> 3, j = lane & 7;
+    const double rq = RHO_EQ * rho;
+    const bool acti = slot_active(h, i);
+    for (int k = 0; k < h.H; ++k) {
+        const double* A = L.al + k * 24;
+        double kd = 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) kd += A[r * 8 + i] * A[r * 8 + j];
+        if (k + 1 < h.H) {
+            const double* B1 = L.be + (k + 1) * 24;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) kd += B1[r * 8 + i] * B1[r * 8 + j];
+        }
+        kd *= rq;
+        if (i == j) kd += SIGMA + (acti ? rho : 1.0);
+        if (k > 0) {
+            const double* B = L.be + k * 24;
+            double ko = 0.0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) ko += A[r * 8 + i] * B[r * 8 + j];
+            ko *= rq;                                     // K_{k,k-1}(i, j)
+            const double* Dp = L.Df + (k - 1) * 64;
+            double lk = 0.0;
+#pragma unroll
+            for (int l = 0; l < 8; ++l) lk += __shfl(ko, i * 8 + l) * Dp[l * 8 + j];
+            L.Lf[k * 64 + lane] = lk;                     // L_k = K_{k,k-1} D_{k-1}^{-1}
+            double s = 0.0;
+#pragma unroll
+            for (int l = 0; l < 8; ++l) s += __shfl(lk, i * 8 + l) * __shfl(ko, j * 8 + l);
+            kd -= s;                                      // D_k = K_kk - L_k K_{k,k-1}'
+        }
+        // in-place Gauss-Jordan sweep inverse of the SPD pivot block
+        double m = kd;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const double piv = __shfl(m, p * 9);
+            const double mip = __shfl(m, i * 8 + p);
+            const double mpj = __shfl(m, p * 8 + j);
+            const double ip = 1.0 / piv;
+            if (i == p && j == p) m = ip;
+            else if (i == p) m = mpj * ip;
+            else if (j == p) m = -mip * ip;
+            else m = m - mip * mpj * ip;
+        }
+        L.Df[k * 64 + lane] = m;
+    }
+    __syncthreads();
+}
+
+// solve KKT x = r in place (r -> x)
+DEV void kkt_solve(const Home& h, const Lds& L, int lane) {
+    const int i = lane >> 3, j = lane & 7;
+    const int H = h.H;
+    for (int k = 0; k < H; ++k) {                          // forward: z_k = r_k - L_k z_{k-1}
+        double s = 0.0;
+        if (k > 0) s = sum8(L.Lf[k * 64 + lane] * L.t1[(k - 1) * 8 + j]);
+        if (j == 0) L.t1[k * 8 + i] = L.r[k * 8 + i] - s;
+        __syncthreads();
+    }
+    for (int k = 0; k < H; ++k) {                          // v_k = D_k^{-1} z_k
+        const double s = sum8(L.Df[k * 64 + lane] * L.t1[k * 8 + j]);
+        if (j == 0) L.t2[k * 8 + i] = s;
+    }
+    __syncthreads();
+    for (int k = H - 1; k >= 0; --k) {                     // backward: x_k = v_k - L_{k+1}' x_{k+1}
+        double s = 0.0;
+        if (k + 1 < H) s = sum8(L.Lf[(k + 1) * 64 + j * 8 + i] * L.r[(k + 1) * 8 + j]);
+        if (j == 0) L.r[k * 8 + i] = L.t2[k * 8 + i] - s;
+        __syncthreads();
+    }
+}
+
+// A_eq' v at element e=(k, jj) for a row vector v[4H]
+DEV double at_times(const Home& h, const Lds& L, const double* v, int k, int jj) {
+    double s = 0.0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) s += L.al[k * 24 + r * 8 + jj] * v[k * RS + r];
+    if (k + 1 < h.H) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) s += L.be[(k + 1) * 24 + r * 8 + jj] * v[(k + 1) * RS + r];
+    }
+    return s;
+}
+// A_eq x at row (k, r) for an element vector x[8H]
+DEV double a_times(const Lds& L, const double* xv, int k, int r) {
+    double s = 0.0;
+#pragma unroll
+    for (int jj = 0; jj < NS; ++jj) s += L.al[k * 24 + r * 8 + jj] * xv[k * 8 + jj];
+    if (k > 0) {
+#pragma unroll
+        for (int jj = 0; jj < NS; ++jj) s += L.be[k * 24 + r * 8 + jj] * xv[(k - 1) * 8 + jj];
+    }
+    return s;
+}
+
+// --------------------------------------------------------------------------------------
+// exact basis polish: from the ADMM point, pick one basic variable per dynamics row
+// (its own state, or the input that drives it), recompute the vertex by forward
+// substitution, the row duals by backward substitution, and check primal bounds and
+// reduced-cost signs.  On success t1 holds the vertex.
+// --------------------------------------------------------------------------------------
+DEV double solve_for(const Lds& L, int k, int r, int bj) {
+    const int o = k * 8;
+    double s = L.beq[k * RS + r];
+    for (int jj = 0; jj < NS; ++jj)
+        if (jj != bj) s -= L.al[k * 24 + r * 8 + jj] * L.t1[o + jj];
+    if (k > 0)
+        for (int jj = 0; jj < NS; ++jj) s -= L.be[k * 24 + r * 8 + jj] * L.t1[o - 8 + jj];
+    return s / L.al[k * 24 + r * 8 + bj];
+}
+
+DEV bool polish(const Home& h, const Lds& L, int lane) {
+    const int H = h.H, n = NS * H;
+    for (int e = lane; e < n; e += WAVE) {
+        const int jj = e & 7;
+        int a = 2;                                          // 2 = inactive slot
+        double v = 0.0;
+        if (slot_active(h, jj)) {
+            const double zb = L.zb[e], yb = L.yb[e];
+            a = (zb - L.lo[e] < -yb) ? -1 : ((L.hi[e] - zb < yb) ? 1 : 0);
+            v = (a == -1) ? L.lo[e] : (a == 1 ? L.hi[e] : L.x[e]);
+        }
+        L.at[e] = a;
+        L.t1[e] = v;
+    }
+    for (int e = lane; e < 4 * (H + 1); e += WAVE) L.lam[e] = 0.0;
+    __syncthreads();
+    if (lane == 0) {
+        int fail = 0;
+        for (int k = 0; k < H && !fail; ++k) {
+            const int o = k * 8;
+            for (int r = 0; r < h.nrows; ++r) {
+                const int own = (r == 0) ? S_T : (r == 1 ? S_TW : S_E);
+                int bj = own;
+                if (L.at[o + own] != 0) {
+                    const int c0 = (r == 0) ? S_U : (r == 1 ? S_W : S_CH);
+                    const int c1 = (r == 2) ? S_DIS : -1;
+                    const bool f0 = L.at[o + c0] == 0, f1 = (c1 >= 0) && L.at[o + c1] == 0;
+                    if (f0 && f1) { fail = 1; break; }
+                    if (f0) bj = c0;
+                    else if (f1) bj = c1;
+                    else {                                  // degenerate: state at bound, try input basic
+                        for (int ci = 0; ci < 2; ++ci) {
+                            const int c = ci == 0 ? c0 : c1;
+                            if (c < 0) continue;
+                            const double v = solve_for(L, k, r, c);
+                            if (v >= L.lo[o + c] - TOL_P * (1 + fabs(L.lo[o + c])) &&
+                                v <= L.hi[o + c] + TOL_P * (1 + fabs(L.hi[o + c]))) { bj = c; break; }
+                        }
+                    }
+                }
+                L.basic[k * RS + r] = bj;
+                L.t1[o + bj] = solve_for(L, k, r, bj);
+            }
+        }
+        if (!fail) {                                        // row duals, backward
+            for (int k = H - 1; k >= 0; --k) {
+                const int o = k * 8;
+                for (int r = h.nrows - 1; r >= 0; --r) {
+                    const int bj = L.basic[k * RS + r];
+                    double s = L.q[o + bj];
+                    for (int r2 = 0; r2 < h.nrows; ++r2) {
+                        if (r2 != r) s += L.al[k * 24 + r2 * 8 + bj] * L.lam[k * RS + r2];
+                        if (k + 1 < H) s += L.be[(k + 1) * 24 + r2 * 8 + bj] * L.lam[(k + 1) * RS + r2];
+                    }
+                    L.lam[k * RS + r] = -s / L.al[k * 24 + r * 8 + bj];
+                }
+            }
+        }
+        L.sc[0] = fail;
+    }
+    __syncthreads();
+    if (L.sc[0] != 0.0) return false;
+    double qmax = 0.0;
+    for (int e = lane; e < n; e += WAVE) qmax = fmax(qmax, fabs(L.q[e]));
+    qmax = wave_max(qmax);
+    bool bad = false;
+    for (int e = lane; e < n; e += WAVE) {
+        const int k = e >> 3, jj = e & 7;
+        const int a = L.at[e];
+        if (a == 2) continue;
+        const double v = L.t1[e];
+        if (v < L.lo[e] - TOL_P * (1 + fabs(L.lo[e])) || v > L.hi[e] + TOL_P * (1 + fabs(L.hi[e]))) bad = true;
+        bool isb = false;
+        for (int r = 0; r < h.nrows; ++r) isb |= (L.basic[k * RS + r] == jj);
+        if (isb) continue;
+        if (a == 0) { bad = true; continue; }
+        const double d = L.q[e] + at_times(h, L, L.lam, k, jj);
+        const double tol = TOL_D * qmax + 1e-14;
+        if ((a == -1 && d < -tol) || (a == 1 && d > tol)) bad = true;
+    }
+    return !wave_any(bad);
+}
+
+// --------------------------------------------------------------------------------------
+// OSQP-style ADMM on  min q'x  s.t.  A_eq x = b,  lo <= x <= hi
+// returns dragg_status; on DRAGG_ST_OPTIMAL, L.x holds the exact vertex
+// --------------------------------------------------------------------------------------
+DEV int admm(const Home& h, const Lds& L, int lane, int max_iter, int check, int* iters) {
+    const int H = h.H, n = NS * H, m = RS * H;
+    double rho = RHO0;
+    for (int e = lane; e < n; e += WAVE) {
+        L.x[e] = 0.0; L.yb[e] = 0.0; L.ybp[e] = 0.0;
+        L.zb[e] = fmin(fmax(0.0, L.lo[e]), L.hi[e]);
+    }
+    for (int e = lane; e < m; e += WAVE) { L.yeq[e] = 0.0; L.yeqp[e] = 0.0; }
+    __syncthreads();
+    factor(h, L, lane, rho);
+    for (int it = 1; it <= max_iter; ++it) {
+        const double rq = RHO_EQ * rho;
+        // rhs = sigma x - q + A_eq'(rq b - y_eq) + (rho z_b - y_b)
+        for (int e = lane; e < m; e += WAVE) {
+            const int r = e & 3;
+            L.zeq[e] = (r < h.nrows) ? rq * L.beq[e] - L.yeq[e] : 0.0;
+        }
+        __syncthreads();
+        for (int e = lane; e < n; e += WAVE) {
+            const int k = e >> 3, jj = e & 7;
+            L.r[e] = slot_active(h, jj)
+                         ? SIGMA * L.x[e] - L.q[e] + at_times(h, L, L.zeq, k, jj) + rho * L.zb[e] - L.yb[e]
+                         : 0.0;
+        }
+        __syncthreads();
+        kkt_solve(h, L, lane);                             // L.r = x~
+        for (int e = lane; e < m; e += WAVE) {
+            const int k = e >> 2, r = e & 3;
+            if (r < h.nrows) {
+                const double zh = a_times(L, L.r, k, r);
+                const double zt = ALPHA * zh + (1 - ALPHA) * L.beq[e];
+                L.yeq[e] += rq * (zt - L.beq[e]);
+            }
+        }
+        for (int e = lane; e < n; e += WAVE) {
+            if (!slot_active(h, e & 7)) continue;
+            const double xt = L.r[e];
+            const double zt = ALPHA * xt + (1 - ALPHA) * L.zb[e];
+            const double zn = fmin(fmax(zt + L.yb[e] / rho, L.lo[e]), L.hi[e]);
+            L.yb[e] += rho * (zt - zn);
+            L.x[e] = ALPHA * xt + (1 - ALPHA) * L.x[e];
+            L.zb[e] = zn;
+        }
+        __syncthreads();
+        if (it % check != 0) continue;
+        if (polish(h, L, lane)) {
+            for (int e = lane; e < n; e += WAVE) L.x[e] = L.t1[e];
+            __syncthreads();
+            *iters = it;
+            return DRAGG_ST_OPTIMAL;
+        }
+        // residuals, infeasibility certificate and rho adaptation
+        double rp = 0, rd = 0, nax = 0, nz = 0, naty = 0, nq = 0, ndy = 0, natdy = 0, supp = 0;
+        for (int e = lane; e < m; e += WAVE) {
+            const int k = e >> 2, r = e & 3;
+            if (r >= h.nrows) { L.zeq[e] = 0.0; continue; }
+            const double ax = a_times(L, L.x, k, r);
+            rp = fmax(rp, fabs(ax - L.beq[e]));
+            nax = fmax(nax, fabs(ax));
+            nz = fmax(nz, fabs(L.beq[e]));
+            const double dy = L.yeq[e] - L.yeqp[e];
+            ndy = fmax(ndy, fabs(dy));
+            supp += L.beq[e] * dy;
+            L.zeq[e] = dy;                                  // reuse as dy_eq
+        }
+        __syncthreads();
+        for (int e = lane; e < n; e += WAVE) {
+            const int k = e >> 3, jj = e & 7;
+            if (!slot_active(h, jj)) continue;
+            rp = fmax(rp, fabs(L.x[e] - L.zb[e]));
+            nax = fmax(nax, fabs(L.x[e]));
+            nz = fmax(nz, fabs(L.zb[e]));
+            const double aty = at_times(h, L, L.yeq, k, jj) + L.yb[e];
+            rd = fmax(rd, fabs(L.q[e] + aty));
+            naty = fmax(naty, fabs(aty));
+            nq = fmax(nq, fabs(L.q[e]));
+            const double dyb = L.yb[e] - L.ybp[e];
+            ndy = fmax(ndy, fabs(dyb));
+            supp += dyb > 0 ? L.hi[e] * dyb : L.lo[e] * dyb;
+            natdy = fmax(natdy, fabs(at_times(h, L, L.zeq, k, jj) + dyb));
+            L.ybp[e] = L.yb[e];
+        }
+        for (int e = lane; e < m; e += WAVE) L.yeqp[e] = L.yeq[e];
+        rp = wave_max(rp); rd = wave_max(rd); nax = wave_max(nax); nz = wave_max(nz);
+        naty = wave_max(naty); nq = wave_max(nq); ndy = wave_max(ndy); natdy = wave_max(natdy);
+        supp = wave_sum(supp);
+        __syncthreads();
+        if (ndy > 1e-12 && natdy < EPS_PINF * ndy && supp < -EPS_PINF * ndy) {
+            *iters = it;
+            return DRAGG_ST_INFEASIBLE_CERT;
+        }
+        const double sp = rp / fmax(fmax(nax, nz), 1e-12);
+        const double sd = rd / fmax(fmax(naty, nq), 1e-12);
+        double nr = rho * sqrt(sp / fmax(sd, 1e-12));
+        nr = fmin(fmax(nr, 1e-6), 1e6);
+        if (nr > 5.0 * rho || nr < 0.2 * rho) {
+            rho = nr;
+            factor(h, L, lane, rho);
+        }
+    }
+    *iters = max_iter;
+    return DRAGG_ST_MAX_ITER;
+}
+
+// --------------------------------------------------------------------------------------
+// integer duty cycles: feasibility-preserving rounding that tracks the relaxed trajectory
+// from the safe side (T_{k+1} >= T*_{k+1} in heating, <= in cooling; Tw likewise)
+// --------------------------------------------------------------------------------------
+DEV bool round_duties(const Home& h, const Lds& L) {
+    double Tk = h.T0, Wk = h.Tw0;
+    for (int k = 0; k < h.H; ++k) {
+        const int o = k * 8;
+        const double bk = L.oat[k + 1] * h.iR * 3600 * h.inv_c;
+        const double uc = (L.x[o + S_T] - h.aT * Tk - bk) / h.g;
+        int u = (int)ceil(uc - 1e-9);
+        u = u < 0 ? 0 : (u > h.S ? h.S : u);
+        double Tn = h.aT * Tk + bk + h.g * u;
+        const double tT = TOL_P * (1 + fabs(h.Tmax));
+        if (Tn < h.Tmin - tT || Tn > h.Tmax + tT) {
+            bool ok = false;
+            for (int d = 1; d <= h.S && !ok; ++d) {
+                for (int sgn = -1; sgn <= 1 && !ok; sgn += 2) {
+                    const int uu = u + sgn * d;
+                    if (uu < 0 || uu > h.S) continue;
+                    const double Tc = h.aT * Tk + bk + h.g * uu;
+                    if (Tc >= h.Tmin - tT && Tc <= h.Tmax + tT) { u = uu; Tn = Tc; ok = true; }
+                }
+            }
+            if (!ok) return false;
+        }
+        const double df = L.draw[k + 1] / h.V;
+        const double rem = 1 - df;
+        const double ck = rem + (-rem * h.iRw) * 3600 * h.inv_w;
+        const double d15 = df * TAP;
+        const double dk = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
+        const double wc = (L.x[o + S_TW] - ck * Wk - h.e * Tn - dk) / h.f;
+        int w = (int)ceil(wc - 1e-9);
+        w = w < 0 ? 0 : (w > h.S ? h.S : w);
+        double Wn = ck * Wk + h.e * Tn + h.f * w + dk;
+        const double wlo = L.lo[o + S_TW], whi = L.hi[o + S_TW];
+        const double tW = TOL_P * (1 + fabs(whi));
+        if (Wn < wlo - tW || Wn > whi + tW) {
+            bool ok = false;
+            for (int d = 1; d <= h.S && !ok; ++d) {
+                for (int sgn = -1; sgn <= 1 && !ok; sgn += 2) {
+                    const int ww = w + sgn * d;
+                    if (ww < 0 || ww > h.S) continue;
+                    const double Wc = ck * Wk + h.e * Tn + h.f * ww + dk;
+                    if (Wc >= wlo - tW && Wc <= whi + tW) { w = ww; Wn = Wc; ok = true; }
+                }
+            }
+            if (!ok) return false;
+        }
+        L.x[o + S_U] = u; L.x[o + S_W] = w; L.x[o + S_T] = Tn; L.x[o + S_TW] = Wn;
+        Tk = Tn; Wk = Wn;
+    }
+    return true;
+}
+
+// closed-form PV curtailment (mpc_calc.py:382-384): u multiplies a cost coefficient
+// gamma^k price_k S A eta ghi_k / 1000, so u = 1 only where that coefficient is negative
+// (u = 0 at a zero coefficient, the lower-bound vertex).
+DEV double pv_curt(const Lds& L, int k) { return (L.price[k] < 0.0 && L.ghi[k] > 0.0) ? 1.0 : 0.0; }
+
+// objective sum_k gamma^k price_k p_grid_k (mpc_calc.py:441-446) for the solution in L.x;
+// also leaves p_grid_k in L.t2[k]
+DEV double objective(const Home& h, const Lds& L, int lane) {
+    double s = 0.0;
+    for (int k = lane; k < h.H; k += WAVE) {
+        const int o = k * 8;
+        const double u = L.x[o + S_U], w = L.x[o + S_W];
+        const double cc = h.winter ? 0.0 : u, hh = h.winter ? u : 0.0;
+        double pl = (h.S * h.Pc) * cc + (h.S * h.Ph) * hh + (h.S * h.Pw) * w;
+        double pg = pl;
+        if (h.batt) pg += h.S * (L.x[o + S_CH] + L.x[o + S_DIS]);
+        if (h.pv) pg -= h.S * (h.pvA * h.pvEta * L.ghi[k] * (1 - pv_curt(L, k)) / 1000);
+        L.t2[k] = pg;
+        s += pow(h.gamma, (double)k) * (L.price[k] * pg);
+    }
+    s = wave_sum(s);
+    __syncthreads();
+    return s;
+}
+
+struct Io {
+    double* vals;          // [NVAL][N]
+    double* fc;            // [NFC][H][N]
+    int N, home;
+    __device__ double& v(int key) const { return vals[(size_t)key * N + home]; }
+    __device__ double& f(int key, int j, int H) const { return fc[((size_t)key * H + j) * N + home]; }
+};
+
+// success branch of cleanup_and_finish (mpc_calc.py:486-526)
+DEV void write_success(const Home& h, const Lds& L, const Io& io, int lane) {
+    const int H = h.H;
+    const double S = h.S;
+    for (int j = lane; j < H; j += WAVE) {
+        const int o = j * 8;
+        const double u = L.x[o + S_U], w = L.x[o + S_W];
+        const double cc = h.winter ? 0.0 : u, hh = h.winter ? u : 0.0;
+        const double pl = (h.S * h.Pc) * cc + (h.S * h.Ph) * hh + (h.S * h.Pw) * w;
+        const double pg = L.t2[j];
+        io.f(DRAGG_K_P_GRID, j, H) = pg / S;
+        io.f(DRAGG_K_FORECAST_P_GRID, j, H) = (j + 1 < H) ? L.t2[j + 1] / S : 0.0;
+        io.f(DRAGG_K_P_LOAD, j, H) = pl / S;
+        io.f(DRAGG_K_TEMP_IN_EV, j, H) = L.x[o + S_T];
+        io.f(DRAGG_K_TEMP_WH_EV, j, H) = L.x[o + S_TW];
+        io.f(DRAGG_K_HVAC_COOL, j, H) = cc / S;
+        io.f(DRAGG_K_HVAC_HEAT, j, H) = hh / S;
+        io.f(DRAGG_K_WH_HEAT, j, H) = w / S;
+        io.f(DRAGG_K_COST, j, H) = L.price[j] * pg;
+        io.f(DRAGG_K_WATERDRAWS, j, H) = L.draw[j];
+        if (h.pv) {
+            const double up = pv_curt(L, j);
+            io.f(DRAGG_K_P_PV, j, H) = h.pvA * h.pvEta * L.ghi[j] * (1 - up) / 1000;
+            io.f(DRAGG_K_U_PV_CURT, j, H) = up;
+        }
+        if (h.batt) {
+            io.f(DRAGG_K_P_BATT_CH, j, H) = L.x[o + S_CH];
+            io.f(DRAGG_K_P_BATT_DISCH, j, H) = L.x[o + S_DIS];
+            io.f(DRAGG_K_E_BATT, j, H) = L.x[o + S_E];
+        }
+        if (j == 0) {          // the un-suffixed fields are the j = 0 values (mpc_calc.py:516)
+            for (int key = 0; key < DRAGG_NFC; ++key) {
+                const bool is_pv = key == DRAGG_K_P_PV || key == DRAGG_K_U_PV_CURT;
+                const bool is_b = key == DRAGG_K_P_BATT_CH || key == DRAGG_K_P_BATT_DISCH || key == DRAGG_K_E_BATT;
+                if ((!is_pv || h.pv) && (!is_b || h.batt)) io.v(key) = io.f(key, 0, H);
+            }
+        }
+    }
+    if (lane == 0) {
+        const double u0 = L.x[S_U], w0 = L.x[S_W];
+        const double c0 = h.winter ? 0.0 : u0, h0 = h.winter ? u0 : 0.0;
+        const double Ts = (h.T0 + ((L.oat[1] - h.T0) * h.iR) * 3600 * h.inv_c) -
+                          (h.Pc * 3600 * h.inv_c) * c0 + (h.Ph * 3600 * h.inv_c) * h0;
+        const double Tws = (h.Tw0 + ((-h.Tw0) * h.iRw) * 3600 * h.inv_w) + h.e * L.x[S_T] + h.f * w0;
+        io.v(DRAGG_V_TEMP_IN_OPT) = Ts;
+        io.v(DRAGG_V_TEMP_WH_OPT) = Tws;
+        io.v(DRAGG_V_CORRECT_SOLVE) = 1.0;
+        io.v(DRAGG_V_SOLVE_COUNTER) = 0.0;
+    }
+}
+
+// failure branch (mpc_calc.py:527-595); returns dragg_status (ERR_PARSE where the
+// reference would raise)
+DEV int write_fallback(const Home& h, const Lds& L, const Io& io, int status) {
+    const int H = h.H;
+    const double S = h.S;
+    int counter = h.counter + 1;
+    const double hmax = h.winter ? S : 0.0, cmax = h.winter ? 0.0 : S;
+    const double hmin = 0.0, cmin = 0.0, whmax = S, whmin = 0.0;
+    const double oat1 = L.oat[1];
+    double heat, cool, wh;
+    double cp_fc[DRAGG_NFC];
+    bool copied = false;
+    if (counter < H && h.t > 0) {                               // :533-557
+        for (int k = 0; k <= DRAGG_K_WATERDRAWS; ++k) cp_fc[k] = io.f(k, counter, H);
+        copied = true;
+        wh = leading_char_value(cp_fc[DRAGG_K_WH_HEAT]);
+        cool = leading_char_value(cp_fc[DRAGG_K_HVAC_COOL]);
+        heat = leading_char_value(cp_fc[DRAGG_K_HVAC_HEAT]);
+        if (wh < 0 || cool < 0 || heat < 0) return DRAGG_ST_ERR_PARSE;
+        const double nT = (double)(h.T0 + 3600 * ((((oat1 - h.T0) / h.R)) - cool * h.Pc + heat * h.Ph) /
+                                              (h.C * h.dt));
+        const double nW = (double)(h.Tw0 + 3600 * ((((nT - h.Tw0) / h.Rw)) + wh * h.Pw) / (h.Cw * h.dt));
+        if (nT > h.Tmax) { heat = hmin; cool = cmax; }
+        else if (nT < h.Tmin) { heat = hmax; cool = cmin; }
+        if (nW < h.Twmin) wh = whmax;
+    } else {                                                    // :559-574
+        counter = counter < H ? H : counter;
+        if (h.T0 > h.Tmax) { heat = hmin; cool = cmax; }
+        else if (h.T0 < h.Tmin) { heat = hmax; cool = cmin; }
+        else { heat = hmin; cool = cmin; }
+        wh = (h.Tw0 < h.Twmin) ? whmax : whmin;
+    }
+    const double nT = h.T0 + 3600 * ((((oat1 - h.T0) / h.R)) - cool * h.Pc + heat * h.Ph) / (h.C * h.dt);
+    const double nW = h.Tw0 + 3600 * (((nT - h.Tw0) / h.Rw) + (wh * h.Pw)) / (h.Cw * h.dt);
+    if (copied) {
+        io.v(DRAGG_K_TEMP_IN_EV) = cp_fc[DRAGG_K_TEMP_IN_EV];
+        io.v(DRAGG_K_TEMP_WH_EV) = cp_fc[DRAGG_K_TEMP_WH_EV];
+    }
+    io.v(DRAGG_V_CORRECT_SOLVE) = 0.0;
+    io.v(DRAGG_K_WH_HEAT) = wh / S;
+    io.v(DRAGG_K_HVAC_HEAT) = heat / S;
+    io.v(DRAGG_K_HVAC_COOL) = cool / S;
+    io.v(DRAGG_V_TEMP_IN_OPT) = nT;
+    io.v(DRAGG_V_TEMP_WH_OPT) = nW;
+    io.v(DRAGG_V_SOLVE_COUNTER) = (double)counter;
+    const double pl = wh * h.Pw + cool * h.Pc + heat * h.Ph;
+    io.v(DRAGG_K_P_LOAD) = pl;
+    io.v(DRAGG_K_FORECAST_P_GRID) = pl;
+    io.v(DRAGG_K_WATERDRAWS) = L.draw[0];
+    io.v(DRAGG_K_P_GRID) = pl;
+    io.v(DRAGG_K_COST) = pl * L.price[0];
+    return status;
+}
+
+struct KArgs {
+    dragg_mpc_dims d;
+    dragg_mpc_problem p;
+    dragg_mpc_explicit ex;
+    double* vals;
+    double* fc;
+    dragg_mpc_out out;
+    const double* noise;
+    int t;
+};
+
+// --------------------------------------------------------------------------------------
+// the kernel: one workgroup (one wave) per home
+// --------------------------------------------------------------------------------------
+template <bool EXPLICIT>
+__global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int home = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int N = a.d.n_homes;
+    if (home >= N) return;
+    Home h;
+    h.H = a.d.horizon; h.S = a.d.sub_steps; h.dt = a.d.dt; h.gamma = a.d.discount;
+    h.type = a.p.home_type[home];
+    h.pv = (h.type & 1) != 0;
+    h.batt = (h.type & 2) != 0;
+    h.nrows = h.batt ? 3 : 2;
+    load_params(h, a.p.params, N, home);
+    const int H = h.H;
+    Lds L = carve(smem, H);
+    Io io{a.vals, a.fc, N, home};
+    int status_pre = -1;
+
+    // ---------------- inputs (get_initial_conditions / set_environmental_variables)
+    if (EXPLICIT) {
+        h.t = a.ex.t[home];
+        h.T0 = a.ex.T0[home]; h.Tw0 = a.ex.Tw0[home]; h.E0 = h.batt ? a.ex.E0[home] : 0.0;
+        h.counter = a.ex.counter[home];
+        h.winter = a.ex.winter[home] != 0;
+        for (int i = lane; i <= H; i += WAVE) {
+            L.draw[i] = a.ex.draw[(size_t)i * N + home];
+            L.oat[i] = a.ex.oat[(size_t)i * N + home];
+            L.ghi[i] = a.ex.ghi[(size_t)i * N + home];
+            L.price[i] = (i < H) ? a.ex.price[(size_t)i * N + home] : 0.0;
+        }
+        __syncthreads();
+    } else {
+        const int t = a.t;
+        h.t = t;
+        const int dt = h.dt;
+        const int lag = H / dt + 1;                           // mpc_calc.py:194
+        const int nraw = lag * dt;
+        const int base_hour = t / dt;
+        const int s0 = a.p.start_index + t;
+        auto rawv = [&](int idx) -> double {                  // np.repeat(list, dt) / dt
+            const int hh = base_hour + idx / dt - lag;
+            const double v = (hh >= 0 && hh < a.d.n_draw_hours) ? a.p.draw_hourly[(size_t)hh * N + home] : 0.0;
+            return v / dt;
+        };
+        for (int i = lane; i <= H; i += WAVE) {
+            double d;
+            if (i < dt) d = rawv(i);
+            else if (i + 1 < nraw) d = ((rawv(i - 1) + rawv(i)) + rawv(i + 1)) / 3.0;
+            else d = (rawv(i - 1) + rawv(i)) / 2.0;
+            L.draw[i] = d;
+            L.oat[i] = a.p.oat[s0 + i];
+            L.ghi[i] = a.p.ghi[s0 + i];
+            const double rp = a.p.reward_price[a.d.n_rp == 1 ? 0 : (i < a.d.n_rp ? i : a.d.n_rp - 1)];
+            L.price[i] = (i < H) ? rp + a.p.tou[s0 + i] : 0.0;
+        }
+        // season draw (mpc_calc.py:220-223, 303-309)
+        double mx = -INFINITY;
+        for (int k = lane; k < H; k += WAVE) {
+            double z;
+            if (a.noise) z = a.noise[(size_t)k * N + home];
+            else {
+                double z0, z1;
+                normal_pair(a.p.seed, home, t, k >> 1, &z0, &z1);
+                z = (k & 1) ? z1 : z0;
+            }
+            mx = fmax(mx, a.p.oat[s0 + k + 1] + pow(1.1, (double)k) * z);
+        }
+        mx = wave_max(mx);
+        mx = fmax(mx, a.p.oat[s0]);
+        h.winter = mx <= 30.0;
+        __syncthreads();
+        const double d0 = L.draw[0];
+        if (t == 0) {
+            h.T0 = h.Tinit;
+            h.Tw0 = (h.Twinit * (h.V - d0) + TAP * d0) / h.V;
+            h.E0 = h.batt ? h.Einit : 0.0;
+            h.counter = 0;
+        } else {
+            const double Tp = io.v(DRAGG_V_TEMP_IN_OPT), Wp = io.v(DRAGG_V_TEMP_WH_OPT);
+            const double cnt = io.v(DRAGG_V_SOLVE_COUNTER);
+            h.T0 = Tp;
+            h.Tw0 = (Wp * (h.V - d0) + TAP * d0) / h.V;
+            h.counter = (int)cnt;
+            h.E0 = h.batt ? io.v(DRAGG_K_E_BATT) : 0.0;
+            bool missing = !(Tp == Tp) || !(Wp == Wp) || !(cnt == cnt);
+            if (h.batt)
+                missing = missing || !(h.E0 == h.E0) || !(io.v(DRAGG_K_P_BATT_CH) == io.v(DRAGG_K_P_BATT_CH)) ||
+                          !(io.v(DRAGG_K_P_BATT_DISCH) == io.v(DRAGG_K_P_BATT_DISCH));
+            if (missing) status_pre = DRAGG_ST_ERR_MISSING;
+        }
+    }
+    if (status_pre == DRAGG_ST_ERR_MISSING) {
+        if (lane == 0) {
+            a.out.status[home] = DRAGG_ST_ERR_MISSING;
+            a.out.iters[home] = 0;
+            a.out.obj[home] = NAN;
+            a.out.relax_obj[home] = NAN;
+        }
+        return;
+    }
+    derive(h);
+    build(h, L, lane);
+
+    // ---------------- solve (solve_mpc)
+    int iters = 0;
+    int status;
+    if (presolve_infeasible(h, L)) status = DRAGG_ST_INFEASIBLE;
+    else {
+        const int mi = a.d.max_iter > 0 ? a.d.max_iter : 4000;
+        const int ce = a.d.check_every > 0 ? a.d.check_every : 10;
+        status = admm(h, L, lane, mi, ce, &iters);
+    }
+    double relax = NAN, obj = NAN;
+    if (status == DRAGG_ST_OPTIMAL) {
+        relax = objective(h, L, lane);
+        if (a.d.int_mode == DRAGG_INT_ROUND) {
+            bool ok = true;
+            if (lane == 0) ok = round_duties(h, L);
+            ok = __shfl(ok ? 1 : 0, 0) != 0;
+            __syncthreads();
+            if (!ok) status = DRAGG_ST_ROUND_FAIL;
+        }
+        if (status == DRAGG_ST_OPTIMAL) obj = objective(h, L, lane);
+    }
+
+    // ---------------- cleanup_and_finish + redis_write_optimal_vals
+    if (status == DRAGG_ST_OPTIMAL) {
+        write_success(h, L, io, lane);
+    } else if (lane == 0) {
+        status = write_fallback(h, L, io, status);
+    }
+    status = __shfl(status, 0);
+    if (lane == 0) {
+        a.out.status[home] = status;
+        a.out.iters[home] = iters;
+        a.out.obj[home] = obj;
+        a.out.relax_obj[home] = relax;
+    }
+    if (a.out.hist && lane == 0)      // lane 0 wrote every vals field of this home
+        for (int k = 0; k < DRAGG_NVAL; ++k) a.out.hist[(size_t)k * N + home] = io.v(k);
+}
+
+__global__ __launch_bounds__(256) void aggregate_kernel(const double* vals, int N, double* out3) {
+    __shared__ double red[3][256];
+    double s[3] = {0, 0, 0};
+    const int keys[3] = {DRAGG_K_P_GRID, DRAGG_K_FORECAST_P_GRID, DRAGG_K_COST};
+    for (int i = threadIdx.x; i < N; i += 256)
+        for (int c = 0; c < 3; ++c) {
+            const double v = vals[(size_t)keys[c] * N + i];
+            if (v == v) s[c] += v;
+        }
+    for (int c = 0; c < 3; ++c) red[c][threadIdx.x] = s[c];
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int c = 0; c < 3; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x < 3) out3[threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ void noise_kernel(int N, int H, uint64_t seed, int t, double* out) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int pairs = (H + 1) / 2;
+    if (idx >= N * pairs) return;
+    const int home = idx % N, pr = idx / N;
+    double z0, z1;
+    normal_pair(seed, home, t, pr, &z0, &z1);
+    out[(size_t)(2 * pr) * N + home] = z0;
+    if (2 * pr + 1 < H) out[(size_t)(2 * pr + 1) * N + home] = z1;
+}
+
+int check_dims(const dragg_mpc_dims* d) {
+    if (!d || d->n_homes < 0 || d->horizon < 1 || d->sub_steps < 1 || d->dt < 1) return DRAGG_E_ARG;
+    if ((size_t)lds_doubles(d->horizon) * 8 > 160 * 1024) return DRAGG_E_HORIZON;
+    return DRAGG_OK;
+}
+
+template <bool EXPLICIT>
+int launch(const KArgs& a, hipStream_t s) {
+    const int H = a.d.horizon;
+    const size_t lds = (size_t)lds_doubles(H) * 8;
+    static bool attr_set[2] = {false, false};
+    if (!attr_set[EXPLICIT ? 1 : 0]) {
+        if (hipFuncSetAttribute((const void*)mpc_home_kernel<EXPLICIT>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+            return DRAGG_E_LDS;
+        attr_set[EXPLICIT ? 1 : 0] = true;
+    }
+    if (a.d.n_homes == 0) return DRAGG_OK;
+    hipLaunchKernelGGL(mpc_home_kernel<EXPLICIT>, dim3(a.d.n_homes), dim3(64), lds, s, a);
+    return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dragg_mpc_abi_version(void) { return DRAGG_MPC_ABI_VERSION; }
+
+const char* dragg_mpc_strerror(int code) {
+    switch (code) {
+        case DRAGG_OK: return "ok";
+        case DRAGG_E_ARG: return "invalid argument";
+        case DRAGG_E_HIP: return "HIP launch error";
+        case DRAGG_E_LDS: return "cannot raise the dynamic LDS limit";
+        case DRAGG_E_HORIZON: return "horizon too long for one workgroup's LDS";
+        default: return "unknown error";
+    }
+}
+
+int dragg_mpc_lds_bytes(const dragg_mpc_dims* dims) {
+    const int rc = check_dims(dims);
+    if (rc) return rc;
+    return lds_doubles(dims->horizon) * 8;
+}
+
+int dragg_mpc_step(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob, dragg_mpc_hash* hash,
+                   dragg_mpc_out* out, int32_t timestep, const double* noise, void* stream) {
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    if (!prob || !hash || !out || timestep < 0 || !prob->params || !prob->home_type || !prob->oat ||
+        !prob->ghi || !prob->tou || !prob->reward_price || !prob->draw_hourly || !hash->vals || !hash->fc ||
+        !out->status || !out->iters || !out->obj || !out->relax_obj)
+        return DRAGG_E_ARG;
+    if (dims->n_rp != 1 && dims->n_rp < dims->horizon) return DRAGG_E_ARG;   // numpy broadcast error
+    if (prob->start_index + timestep + dims->horizon >= dims->n_env) return DRAGG_E_ARG;
+    KArgs a{};
+    a.d = *dims; a.p = *prob; a.vals = hash->vals; a.fc = hash->fc; a.out = *out; a.noise = noise;
+    a.t = timestep;
+    return launch<false>(a, (hipStream_t)stream);
+}
+
+int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob,
+                             const dragg_mpc_explicit* in, dragg_mpc_hash* hash, dragg_mpc_out* out,
+                             void* stream) {
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    if (!prob || !in || !hash || !out || !prob->params || !prob->home_type || !in->t || !in->T0 ||
+        !in->Tw0 || !in->E0 || !in->counter || !in->winter || !in->draw || !in->oat || !in->ghi ||
+        !in->price || !hash->vals || !hash->fc || !out->status || !out->iters || !out->obj ||
+        !out->relax_obj)
+        return DRAGG_E_ARG;
+    KArgs a{};
+    a.d = *dims; a.p = *prob; a.ex = *in; a.vals = hash->vals; a.fc = hash->fc; a.out = *out;
+    return launch<true>(a, (hipStream_t)stream);
+}
+
+int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, double* out3, void* stream) {
+    if (!dims || !hash || !hash->vals || !out3 || dims->n_homes < 0) return DRAGG_E_ARG;
+    hipLaunchKernelGGL(aggregate_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, hash->vals,
+                       dims->n_homes, out3);
+    return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
+}
+
+int dragg_mpc_season_noise(const dragg_mpc_dims* dims, uint64_t seed, int32_t timestep, double* noise_out,
+                           void* stream) {
+    if (!dims || !noise_out || dims->n_homes < 0 || dims->horizon < 1) return DRAGG_E_ARG;
+    const int total = dims->n_homes * ((dims->horizon + 1) / 2);
+    if (total == 0) return DRAGG_OK;
+    hipLaunchKernelGGL(noise_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       dims->n_homes, dims->horizon, seed, timestep, noise_out);
+    return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
+}
+
+}  // extern "C"

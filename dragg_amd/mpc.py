@@ -1,0 +1,229 @@
+"""Host side of the batched MPC: home packing, device-resident hash arrays, launches.
+
+This is the MI355X-native replacement of `dragg/mpc_calc.py`'s per-home solve: all homes
+of a timestep are solved by ONE kernel launch of libdragg_mi355x.so (one 64-lane
+workgroup per home).  Per-home parameters, the redis "hash" of each home and the
+environment lists live on the GPU as fp64 struct-of-arrays tensors (home index
+innermost).  See `dragg_amd.calc.MPCCalc` for the per-home facade with the
+reference's interface.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+TAP_TEMP = 15.0  # mpc_calc.py:181
+
+
+def _f(x):
+    return float(x)
+
+
+def hems_dims(home):
+    """(S, dt, H, discount) exactly as `setup_base_problem` derives them (mpc_calc.py:148-152)."""
+    hems = home["hems"]
+    S = max(1, int(hems["sub_subhourly_steps"]))
+    dt = max(1, int(hems["hourly_agg_steps"]))
+    H = max(1, int(hems["horizon"] * dt))
+    return S, dt, H, float(hems["discount_factor"])
+
+
+def pack_homes(homes):
+    """home dicts (aggregator.py:423-449 schema) -> (params [NPARAM][N], types [N], draws [hours][N], dims).
+
+    Derived constants are computed with the reference's own float expressions
+    (mpc_calc.py:157-189, 239-244, 257-258, 274)."""
+    N = len(homes)
+    if N == 0:
+        raise ValueError("no homes")
+    S, dt, H, disc = hems_dims(homes[0])
+    for h in homes:
+        if hems_dims(h) != (S, dt, H, disc):
+            raise ValueError("all homes of a batch must share the hems settings (responsive_hems)")
+    P = np.zeros((L.NPARAM, N))
+    types = np.zeros(N, dtype=np.int32)
+    nd = max(len(h["wh"]["draw_sizes"]) for h in homes)
+    draws = np.zeros((nd, N))
+    for i, h in enumerate(homes):
+        if h["type"] not in L.TYPE_CODE:
+            raise ValueError(f"unknown home type {h['type']!r}")
+        types[i] = L.TYPE_CODE[h["type"]]
+        hv, wh = h["hvac"], h["wh"]
+        P[L.P["R"], i] = _f(hv["r"])
+        P[L.P["C"], i] = _f(hv["c"]) * 1000
+        P[L.P["PC"], i] = _f(hv["p_c"]) / S
+        P[L.P["PH"], i] = (_f(hv["p_h"])) / S
+        P[L.P["RW"], i] = _f(wh["r"]) * 1000
+        P[L.P["PW"], i] = _f(wh["p"]) / S
+        P[L.P["CW"], i] = _f(wh["tank_size"]) * 4.2
+        P[L.P["V"], i] = _f(wh["tank_size"])
+        P[L.P["TMIN"], i] = _f(hv["temp_in_min"])
+        P[L.P["TMAX"], i] = _f(hv["temp_in_max"])
+        P[L.P["TWMIN"], i] = _f(wh["temp_wh_min"])
+        P[L.P["TWMAX"], i] = _f(wh["temp_wh_max"])
+        P[L.P["TINIT"], i] = _f(hv["temp_in_init"])
+        P[L.P["TWINIT"], i] = _f(wh["temp_wh_init"])
+        if "battery" in h["type"]:
+            b = h["battery"]
+            cap = _f(b["capacity"])
+            P[L.P["BRATE"], i] = _f(b["max_rate"])
+            P[L.P["EMIN"], i] = _f(b["capacity_lower"]) * cap
+            P[L.P["EMAX"], i] = _f(b["capacity_upper"]) * cap
+            P[L.P["ETAC"], i] = _f(b["ch_eff"])
+            P[L.P["ETAD"], i] = _f(b["disch_eff"])
+            P[L.P["EINIT"], i] = _f(b["e_batt_init"]) * cap
+        if "pv" in h["type"]:
+            P[L.P["PVAREA"], i] = _f(h["pv"]["area"])
+            P[L.P["PVEFF"], i] = _f(h["pv"]["eff"])
+        ds = np.asarray(h["wh"]["draw_sizes"], dtype=float)
+        draws[:len(ds), i] = ds
+    return P, types, draws, dict(S=S, dt=dt, H=H, discount=disc, n_draw_hours=nd)
+
+
+class MPCBatch:
+    """A device-resident batch of homes that share one environment.
+
+    Parameters
+    ----------
+    homes : list of home dicts (the `all_homes` records of the aggregator).
+    oat, ghi, tou : full-length redis lists (aggregator.py:653-662), any sequence of floats.
+    start_index : `start_hour_index` (aggregator.py:630-638).
+    reward_price : the redis 'reward_price' list (length 1 or >= H, mpc_calc.py:353).
+    int_mode : 'round' (relaxation + feasible rounding of the integer duty cycles) or 'relax'.
+    seed : key of the on-device season-noise stream used when no noise is supplied.
+    """
+
+    def __init__(self, homes, oat=None, ghi=None, tou=None, start_index=0, reward_price=(0.0,),
+                 int_mode="round", seed=0, max_iter=4000, check_every=10, device="cuda"):
+        self.lib = L.load()
+        if not torch.cuda.is_available():
+            raise L.DraggError("no GPU visible: the batched MPC has no CPU fallback")
+        self.device = torch.device(device)
+        self.homes = homes
+        self.names = [h["name"] for h in homes]
+        P, types, draws, dm = pack_homes(homes)
+        self.N, self.H, self.S, self.dt = len(homes), dm["H"], dm["S"], dm["dt"]
+        dev = self.device
+        self.params = torch.tensor(P, dtype=torch.float64, device=dev).contiguous()
+        self.types = torch.tensor(types, dtype=torch.int32, device=dev)
+        self.types_host = types
+        self.draws = torch.tensor(draws, dtype=torch.float64, device=dev).contiguous()
+        self.dims = L.Dims(n_homes=self.N, horizon=self.H, sub_steps=self.S, dt=self.dt,
+                           n_draw_hours=dm["n_draw_hours"], n_env=0, n_rp=1,
+                           int_mode=L.INT_ROUND if int_mode == "round" else L.INT_RELAX,
+                           max_iter=max_iter, check_every=check_every, discount=dm["discount"])
+        self.seed = int(seed)
+        self.set_environment(oat if oat is not None else [0.0], ghi if ghi is not None else [0.0],
+                             tou if tou is not None else [0.0], start_index)
+        self.set_reward_price(reward_price)
+        self.vals = torch.full((L.NVAL, self.N), float("nan"), dtype=torch.float64, device=dev)
+        self.fc = torch.full((L.NFC, self.H, self.N), float("nan"), dtype=torch.float64, device=dev)
+        self.status = torch.zeros(self.N, dtype=torch.int32, device=dev)
+        self.iters = torch.zeros(self.N, dtype=torch.int32, device=dev)
+        self.obj = torch.zeros(self.N, dtype=torch.float64, device=dev)
+        self.relax_obj = torch.zeros(self.N, dtype=torch.float64, device=dev)
+        self.agg = torch.zeros(3, dtype=torch.float64, device=dev)
+        rc = self.lib.dragg_mpc_lds_bytes(ctypes.byref(self.dims))
+        if rc < 0:
+            L.check(rc)
+        self.lds_bytes = rc
+
+    # ------------------------------------------------------------------ environment
+    def set_environment(self, oat, ghi, tou, start_index):
+        dev = self.device
+        self.oat = torch.tensor(np.asarray(oat, dtype=float), dtype=torch.float64, device=dev)
+        self.ghi = torch.tensor(np.asarray(ghi, dtype=float), dtype=torch.float64, device=dev)
+        self.tou = torch.tensor(np.asarray(tou, dtype=float), dtype=torch.float64, device=dev)
+        self.start_index = int(start_index)
+        self.dims.n_env = int(min(len(oat), len(ghi), len(tou)))
+
+    def set_reward_price(self, rp):
+        rp = np.asarray([float(v) for v in rp], dtype=float)
+        if len(rp) != 1 and len(rp) < self.H:
+            # np.array(rp[:H]) + tou[:H] raises in the reference (mpc_calc.py:353)
+            raise ValueError(f"operands could not be broadcast together: reward_price has {len(rp)} "
+                             f"entries, horizon is {self.H}")
+        self.rp = torch.tensor(rp, dtype=torch.float64, device=self.device)
+        self.dims.n_rp = len(rp)
+
+    # ------------------------------------------------------------------ structs
+    def _problem(self):
+        return L.Problem(params=L.ptr(self.params), home_type=L.ptr(self.types), draw_hourly=L.ptr(self.draws),
+                         oat=L.ptr(self.oat), ghi=L.ptr(self.ghi), tou=L.ptr(self.tou),
+                         reward_price=L.ptr(self.rp), start_index=self.start_index, seed=self.seed)
+
+    def _hash(self):
+        return L.Hash(vals=L.ptr(self.vals), fc=L.ptr(self.fc))
+
+    def _out(self, hist=None):
+        return L.Out(status=L.ptr(self.status), iters=L.ptr(self.iters), obj=L.ptr(self.obj),
+                     relax_obj=L.ptr(self.relax_obj), hist=L.ptr(hist))
+
+    # ------------------------------------------------------------------ launches
+    def step(self, t, noise=None, hist=None, stream=None):
+        """One closed-loop timestep for every home (run_iteration, aggregator.py:711-726)."""
+        if noise is not None:
+            noise = noise.to(device=self.device, dtype=torch.float64).contiguous()
+            assert tuple(noise.shape) == (self.H, self.N)
+        prob, hsh, out = self._problem(), self._hash(), self._out(hist)
+        L.check(self.lib.dragg_mpc_step(ctypes.byref(self.dims), ctypes.byref(prob), ctypes.byref(hsh),
+                                        ctypes.byref(out), int(t), L.ptr(noise), L.stream_ptr(stream)))
+        self._keep = (noise, hist)
+        return self.status
+
+    def solve_explicit(self, t, T0, Tw0, E0, counter, winter, draw, oat, ghi, price, stream=None):
+        """Independent per-home solves with explicit inputs ([N] and [H+1 or H][N] arrays)."""
+        dev, N, H = self.device, self.N, self.H
+
+        def d(x, shape, dtype=torch.float64):
+            tt = torch.as_tensor(np.asarray(x), dtype=dtype).to(dev).reshape(shape).contiguous()
+            return tt
+        ex_t = {
+            "t": d(t, (N,), torch.int32), "T0": d(T0, (N,)), "Tw0": d(Tw0, (N,)),
+            "E0": d(np.nan_to_num(np.asarray(E0, dtype=float)), (N,)),
+            "counter": d(counter, (N,), torch.int32), "winter": d(winter, (N,), torch.int32),
+            "draw": d(draw, (H + 1, N)), "oat": d(oat, (H + 1, N)), "ghi": d(ghi, (H + 1, N)),
+            "price": d(price, (H, N)),
+        }
+        ex = L.Explicit(**{k: L.ptr(v) for k, v in ex_t.items()})
+        prob, hsh, out = self._problem(), self._hash(), self._out()
+        L.check(self.lib.dragg_mpc_solve_explicit(ctypes.byref(self.dims), ctypes.byref(prob), ctypes.byref(ex),
+                                                  ctypes.byref(hsh), ctypes.byref(out), L.stream_ptr(stream)))
+        self._keep = ex_t
+        return self.status
+
+    def aggregate(self, stream=None):
+        """collect_data sums (aggregator.py:751-753) -> device tensor [agg_load, forecast_load, agg_cost]."""
+        hsh = self._hash()
+        L.check(self.lib.dragg_mpc_aggregate(ctypes.byref(self.dims), ctypes.byref(hsh), L.ptr(self.agg),
+                                             L.stream_ptr(stream)))
+        return self.agg
+
+    def season_noise(self, t, stream=None):
+        out = torch.empty((self.H, self.N), dtype=torch.float64, device=self.device)
+        L.check(self.lib.dragg_mpc_season_noise(ctypes.byref(self.dims), self.seed, int(t), L.ptr(out),
+                                                L.stream_ptr(stream)))
+        return out
+
+    # ------------------------------------------------------------------ hash views
+    def hash_dict(self, i, as_str=True):
+        """The home's redis hash as `hgetall` would return it (str values, absent fields omitted)."""
+        vals = self.vals[:, i].cpu().numpy()
+        fc = self.fc[:, :, i].cpu().numpy()
+        out = {}
+        for k, name in enumerate(L.FC_KEYS):
+            for j in range(self.H):
+                if not np.isnan(fc[k, j]):
+                    out[f"{name}_{j}"] = fc[k, j]
+        for k, name in enumerate(L.VAL_KEYS):
+            if not np.isnan(vals[k]):
+                out[name] = vals[k]
+        if "solve_counter" in out:
+            out["solve_counter"] = int(out["solve_counter"])
+        if "correct_solve" in out:
+            out["correct_solve"] = int(out["correct_solve"])
+        if as_str:
+            out = {k: (str(v) if isinstance(v, int) else repr(float(v))) for k, v in out.items()}
+        return out

@@ -1,0 +1,196 @@
+/*
+ * dragg_mi355x.h -- C ABI of the batched MI355X (gfx950) home-MPC solver.
+ *
+ * Drop-in replacement for the per-home HEMS solve of corymosiman12/dragg:
+ *
+ *   reference                                   this ABI
+ *   -----------------------------------------   ------------------------------------------
+ *   MPCCalc.run_home()        mpc_calc.py:649   dragg_mpc_step()      (device-resident state)
+ *     get_initial_conditions  mpc_calc.py:264     (initial state read from the hash arrays)
+ *     water_draws             mpc_calc.py:193     (computed on device from draw_hourly)
+ *     set_environmental_vars  mpc_calc.py:206     (slices of oat/ghi/tou + reward price)
+ *     add_*_constraints       mpc_calc.py:291-432 (built on device, never materialised)
+ *     solve_mpc (GLPK_MI)     mpc_calc.py:434     (batched banded-KKT ADMM + exact polish)
+ *     cleanup_and_finish      mpc_calc.py:476     (success extraction / fallback thermostat)
+ *     redis_write_optimal_vals mpc_calc.py:100    (hash arrays updated in place)
+ *   manage_home + ProcessPool aggregator.py:723   one launch over all homes of a timestep
+ *   collect_data sums         aggregator.py:751   dragg_mpc_aggregate()
+ *   MPCCalc per-solve (explicit inputs)         dragg_mpc_solve_explicit()
+ *
+ * Conventions
+ *  - Every pointer in the structs below is a DEVICE pointer (hipMalloc / torch
+ *    CUDA tensors), fp64 unless stated; arrays are struct-of-arrays with the home
+ *    index innermost: element (f, h) of a [F][N] array lives at f*N + h.
+ *  - All entry points return 0 on success or a negative dragg_mpc_error code;
+ *    nothing throws across the ABI.  Launches are asynchronous on `stream`
+ *    (a hipStream_t, NULL = default stream); no host synchronisation inside.
+ *  - The per-home redis hash (`redis_client.py`, all values str) is replaced by
+ *    two fp64 arrays: `vals` [DRAGG_NVAL][N] (the scalar fields a step writes)
+ *    and `fc` [DRAGG_NFC][H][N] (the `<key>_<j>` forecast fields, rewritten only
+ *    by a successful solve).  NaN means "field absent from the hash".
+ */
+#ifndef DRAGG_MI355X_H
+#define DRAGG_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DRAGG_MPC_ABI_VERSION 1
+
+/* home types (aggregator.py:425, 468, 520, 555); bit 0 = pv, bit 1 = battery */
+enum dragg_home_type {
+    DRAGG_BASE = 0, DRAGG_PV_ONLY = 1, DRAGG_BATTERY_ONLY = 2, DRAGG_PV_BATTERY = 3
+};
+
+/* per-home parameters, rows of params[DRAGG_NPARAM][N] (mpc_calc.py:157-189, 239-258) */
+enum dragg_param {
+    DRAGG_P_R = 0,        /* hvac.r                               */
+    DRAGG_P_C,            /* hvac.c * 1000                        */
+    DRAGG_P_PC,           /* hvac.p_c / S                         */
+    DRAGG_P_PH,           /* hvac.p_h / S                         */
+    DRAGG_P_RW,           /* wh.r * 1000                          */
+    DRAGG_P_PW,           /* wh.p / S                             */
+    DRAGG_P_CW,           /* wh.tank_size * 4.2                   */
+    DRAGG_P_V,            /* wh.tank_size                         */
+    DRAGG_P_TMIN, DRAGG_P_TMAX, DRAGG_P_TWMIN, DRAGG_P_TWMAX,
+    DRAGG_P_TINIT,        /* hvac.temp_in_init                    */
+    DRAGG_P_TWINIT,       /* wh.temp_wh_init                      */
+    DRAGG_P_BRATE,        /* battery.max_rate                     */
+    DRAGG_P_EMIN,         /* battery.capacity_lower * capacity    */
+    DRAGG_P_EMAX,         /* battery.capacity_upper * capacity    */
+    DRAGG_P_ETAC, DRAGG_P_ETAD,
+    DRAGG_P_EINIT,        /* battery.e_batt_init * capacity       */
+    DRAGG_P_PVAREA, DRAGG_P_PVEFF,
+    DRAGG_NPARAM
+};
+
+/* forecast keys: rows of fc[DRAGG_NFC][H][N] (`<key>_<j>` hash fields, mpc_calc.py:514-520) */
+enum dragg_fc_key {
+    DRAGG_K_P_GRID = 0, DRAGG_K_FORECAST_P_GRID, DRAGG_K_P_LOAD, DRAGG_K_TEMP_IN_EV,
+    DRAGG_K_TEMP_WH_EV, DRAGG_K_HVAC_COOL, DRAGG_K_HVAC_HEAT, DRAGG_K_WH_HEAT, DRAGG_K_COST,
+    DRAGG_K_WATERDRAWS, DRAGG_K_P_PV, DRAGG_K_U_PV_CURT, DRAGG_K_P_BATT_CH,
+    DRAGG_K_P_BATT_DISCH, DRAGG_K_E_BATT,
+    DRAGG_NFC
+};
+
+/* scalar hash fields: rows of vals[DRAGG_NVAL][N]; rows 0..14 are the keys above, i.e. the
+   un-suffixed `<key>` field (mpc_calc.py:516, 584-594) */
+enum dragg_val {
+    DRAGG_V_TEMP_IN_OPT = DRAGG_NFC, DRAGG_V_TEMP_WH_OPT, DRAGG_V_CORRECT_SOLVE,
+    DRAGG_V_SOLVE_COUNTER,
+    DRAGG_NVAL
+};
+
+/* per-home status written by a step (status[N]) */
+enum dragg_status {
+    DRAGG_ST_OPTIMAL = 0,          /* LP optimal (exact vertex) and integer rounding succeeded  */
+    DRAGG_ST_INFEASIBLE = 1,       /* proven infeasible by interval presolve                   */
+    DRAGG_ST_INFEASIBLE_CERT = 2,  /* ADMM primal-infeasibility certificate                     */
+    DRAGG_ST_MAX_ITER = 3,         /* no verified vertex within max_iter                         */
+    DRAGG_ST_ROUND_FAIL = 4,       /* relaxation optimal, no integer duty schedule found         */
+    DRAGG_ST_ERR_PARSE = 5,        /* fallback's float(str[0]) would raise (mpc_calc.py:537)     */
+    DRAGG_ST_ERR_MISSING = 6       /* hash field missing at t>0 (KeyError, mpc_calc.py:280-289)  */
+};
+
+enum dragg_mpc_error {
+    DRAGG_OK = 0, DRAGG_E_ARG = -1, DRAGG_E_HIP = -2, DRAGG_E_LDS = -3, DRAGG_E_HORIZON = -4
+};
+
+/* integer handling of the duty-cycle variables (mpc_calc.py:171-173) */
+enum dragg_int_mode {
+    DRAGG_INT_ROUND = 0,   /* relaxation + feasibility-preserving rounding (default)  */
+    DRAGG_INT_RELAX = 1    /* report the LP relaxation                                */
+};
+
+typedef struct dragg_mpc_dims {
+    int32_t n_homes;       /* N                                                        */
+    int32_t horizon;       /* H = prediction_horizon * dt            (mpc_calc.py:150) */
+    int32_t sub_steps;     /* S = sub_subhourly_steps                (mpc_calc.py:148) */
+    int32_t dt;            /* hourly_agg_steps                       (mpc_calc.py:149) */
+    int32_t n_draw_hours;  /* columns of draw_hourly                                   */
+    int32_t n_env;         /* length of oat/ghi/tou                                    */
+    int32_t n_rp;          /* length of reward_price (1 or >= H, mpc_calc.py:353)      */
+    int32_t int_mode;      /* dragg_int_mode                                           */
+    int32_t max_iter;      /* ADMM iteration cap (<=0: default 4000)                   */
+    int32_t check_every;   /* polish / residual check interval (<=0: default 10)       */
+    double discount;       /* discount_factor                        (mpc_calc.py:152) */
+} dragg_mpc_dims;
+
+typedef struct dragg_mpc_problem {
+    const double* params;       /* [DRAGG_NPARAM][N]                                    */
+    const int32_t* home_type;   /* [N] dragg_home_type                                  */
+    const double* draw_hourly;  /* [n_draw_hours][N] wh.draw_sizes (aggregator.py:377)  */
+    const double* oat;          /* [n_env] redis 'OAT' list                             */
+    const double* ghi;          /* [n_env] redis 'GHI' list                             */
+    const double* tou;          /* [n_env] redis 'tou' list                             */
+    const double* reward_price; /* [n_rp]  redis 'reward_price' list                    */
+    int32_t start_index;        /* start_hour_index (aggregator.py:630-638)             */
+    int32_t _pad;
+    uint64_t seed;              /* keyed season-noise stream when noise == NULL         */
+} dragg_mpc_problem;
+
+typedef struct dragg_mpc_hash {
+    double* vals;               /* [DRAGG_NVAL][N]  in/out, NaN = absent               */
+    double* fc;                 /* [DRAGG_NFC][H][N] in/out                            */
+} dragg_mpc_hash;
+
+typedef struct dragg_mpc_out {
+    int32_t* status;            /* [N] dragg_status                                     */
+    int32_t* iters;             /* [N] ADMM iterations used (0 if presolve decided)    */
+    double* obj;                /* [N] objective sum_k gamma^k price_k p_grid_k         */
+    double* relax_obj;          /* [N] LP-relaxation objective (NaN if infeasible)     */
+    double* hist;               /* optional [DRAGG_NVAL][N] copy of vals after the step */
+} dragg_mpc_out;
+
+/* explicit per-solve inputs (parity tests and the per-home MPCCalc facade) */
+typedef struct dragg_mpc_explicit {
+    const int32_t* t;           /* [N] timestep (fallback rule needs t > 0)             */
+    const double* T0;           /* [N] temp_in_init value                               */
+    const double* Tw0;          /* [N] temp_wh_init value (after draw mixing)           */
+    const double* E0;           /* [N] e_batt_init value (ignored for non-battery)      */
+    const int32_t* counter;     /* [N] solve_counter read from the hash                 */
+    const int32_t* winter;      /* [N] 1 = max(oat_ev) <= 30 (mpc_calc.py:303)          */
+    const double* draw;         /* [H+1][N] draw_size                                   */
+    const double* oat;          /* [H+1][N] oat_current                                 */
+    const double* ghi;          /* [H+1][N] ghi_current                                 */
+    const double* price;        /* [H][N]   total_price                                 */
+} dragg_mpc_explicit;
+
+int dragg_mpc_abi_version(void);
+const char* dragg_mpc_strerror(int code);
+
+/* Dynamic LDS bytes one home (workgroup) needs for this horizon; < 0 if H unsupported. */
+int dragg_mpc_lds_bytes(const dragg_mpc_dims* dims);
+
+/* One closed-loop timestep for all N homes: reads the hash arrays (t > 0) or the
+   parameters (t == 0), solves, and writes the hash arrays back in place.
+   noise: [H][N] standard normals for the season draw (mpc_calc.py:222) or NULL for the
+   keyed on-device stream philox(seed, home, t). */
+int dragg_mpc_step(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob,
+                   dragg_mpc_hash* hash, dragg_mpc_out* out, int32_t timestep,
+                   const double* noise, void* stream);
+
+/* Independent solves with explicit inputs; hash supplies the fallback's forecast fields
+   and receives the written fields exactly as in dragg_mpc_step. prob->oat/ghi/tou/
+   reward_price/draw_hourly are ignored. */
+int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob,
+                             const dragg_mpc_explicit* in, dragg_mpc_hash* hash,
+                             dragg_mpc_out* out, void* stream);
+
+/* collect_data sums (aggregator.py:751-753): out3 = {sum p_grid_opt, sum
+   forecast_p_grid_opt, sum cost_opt} over homes whose fields are present. */
+int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, double* out3,
+                        void* stream);
+
+/* The keyed season-noise stream used when noise == NULL: writes [H][N] normals for
+   timestep t (exposed so the host and tests can reproduce the draw). */
+int dragg_mpc_season_noise(const dragg_mpc_dims* dims, uint64_t seed, int32_t timestep,
+                           double* noise_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRAGG_MI355X_H */
