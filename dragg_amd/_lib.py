@@ -48,7 +48,7 @@ class Dims(ctypes.Structure):
 class Problem(ctypes.Structure):
     _fields_ = [("params", c_dp), ("home_type", c_dp), ("draw_hourly", c_dp), ("oat", c_dp), ("ghi", c_dp),
                 ("tou", c_dp), ("reward_price", c_dp), ("start_index", ctypes.c_int32),
-                ("_pad", ctypes.c_int32), ("seed", ctypes.c_uint64)]
+                ("home_offset", ctypes.c_int32), ("seed", ctypes.c_uint64)]
 
 
 class Hash(ctypes.Structure):
@@ -93,7 +93,8 @@ def load(path=LIB_PATH):
                                              ctypes.POINTER(Explicit), ctypes.POINTER(Hash),
                                              ctypes.POINTER(Out), c_dp]
     lib.dragg_mpc_aggregate.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Hash), c_dp, c_dp]
-    lib.dragg_mpc_season_noise.argtypes = [ctypes.POINTER(Dims), ctypes.c_uint64, ctypes.c_int32, c_dp, c_dp]
+    lib.dragg_mpc_season_noise.argtypes = [ctypes.POINTER(Dims), ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
+                                           c_dp, c_dp]
     if lib.dragg_mpc_abi_version() != ABI_VERSION:
         raise DraggError("ABI version mismatch between dragg_amd and libdragg_mi355x.so")
     _LIB = lib

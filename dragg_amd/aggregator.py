@@ -1,0 +1,111 @@
+"""Device-resident replacement of the aggregator's per-timestep loop.
+
+Reference: `Aggregator.run_baseline / run_iteration / collect_data`
+(aggregator.py:711-778).  There, every timestep forks a process pool, pickles each
+MPCCalc to a worker, round-trips ~400 redis fields per home and sums three fields per
+home on the host.  Here the community's state never leaves the GPU:
+
+* one `dragg_mpc_step` launch solves and advances every home of this rank's shard;
+* `dragg_mpc_aggregate` reduces agg_load / forecast_load / agg_cost on device and, with
+  more than one rank, a single 24-byte RCCL all-reduce (torch.distributed, backend
+  "nccl" = RCCL over xGMI) combines the shards -- the only cross-GPU traffic;
+* the per-step hash fields are appended to an on-device history (the
+  `collected_data` lists), converted to the results.json layout only on request.
+
+Homes are sharded in contiguous blocks of the global community order; the season-noise
+stream is keyed by the GLOBAL home index, so results do not depend on the shard layout.
+"""
+import numpy as np
+import torch
+
+from . import _lib as L
+from .mpc import MPCBatch
+
+
+def shard_bounds(n, rank, world):
+    return (n * rank) // world, (n * (rank + 1)) // world
+
+
+class DeviceAggregator:
+    def __init__(self, homes, oat, ghi, tou, start_index=0, num_timesteps=96, reward_price=(0.0,),
+                 int_mode="round", seed=0, rank=0, world=1, group=None, keep_history=True,
+                 max_iter=4000, check_every=10, device=None):
+        self.rank, self.world, self.group = rank, world, group
+        lo, hi = shard_bounds(len(homes), rank, world)
+        self.lo, self.hi = lo, hi
+        self.all_homes = homes
+        self.homes = homes[lo:hi]
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        self.batch = MPCBatch(self.homes, oat, ghi, tou, start_index, reward_price, int_mode=int_mode,
+                              seed=seed, home_offset=lo, max_iter=max_iter, check_every=check_every,
+                              device=dev)
+        self.num_timesteps = num_timesteps
+        self.timestep = 0
+        n = self.batch.N
+        self.hist = (torch.full((num_timesteps, L.NVAL, n), float("nan"), dtype=torch.float64, device=dev)
+                     if keep_history else None)
+        self.agg_hist = torch.zeros((num_timesteps, 3), dtype=torch.float64, device=dev)
+        self.status_hist = torch.zeros((num_timesteps, n), dtype=torch.int8, device=dev)
+
+    # aggregator.py:711-726
+    def run_iteration(self, noise=None):
+        t = self.timestep
+        hist = self.hist[t] if self.hist is not None else None
+        self.batch.step(t, noise=noise, hist=hist)
+        self.status_hist[t].copy_(self.batch.status, non_blocking=True)
+        self.timestep += 1
+
+    # aggregator.py:728-755 (sums only; the per-home series stay in self.hist)
+    def collect_data(self):
+        t = self.timestep - 1
+        agg = self.batch.aggregate()
+        if self.world > 1:
+            torch.distributed.all_reduce(agg, group=self.group)
+        self.agg_hist[t].copy_(agg)
+        return agg
+
+    # aggregator.py:757-778
+    def run_baseline(self, steps=None, noise_fn=None):
+        steps = self.num_timesteps - self.timestep if steps is None else steps
+        for _ in range(steps):
+            self.run_iteration(noise_fn(self.timestep) if noise_fn else None)
+            self.collect_data()
+        return self.agg_hist[:self.timestep]
+
+    def check_errors(self):
+        """Raise as the reference would if a home hit a crashing path (KeyError / ValueError)."""
+        st = self.status_hist[:self.timestep].cpu().numpy()
+        for code, exc in ((L.ST_ERR_MISSING, KeyError), (L.ST_ERR_PARSE, ValueError)):
+            bad = np.argwhere(st == code)
+            if len(bad):
+                t, i = bad[0]
+                raise exc(f"home {self.homes[i]['name']} at timestep {t}: {L.STATUS_NAMES[code]} "
+                          "(the reference raises here, mpc_calc.py:280-289 / 537-539)")
+
+    def collected_data(self):
+        """This shard's `collected_data` dict (aggregator.py:589-615, 737-748 append order)."""
+        keys = ["p_grid_opt", "forecast_p_grid_opt", "p_load_opt", "temp_in_opt", "temp_wh_opt",
+                "hvac_cool_on_opt", "hvac_heat_on_opt", "wh_heat_on_opt", "cost_opt", "waterdraws",
+                "correct_solve"]
+        hist = self.hist[:self.timestep].cpu().numpy()
+        out = {}
+        for i, h in enumerate(self.homes):
+            d = {"type": h["type"], "temp_in_sp": h["hvac"]["temp_in_sp"], "temp_wh_sp": h["wh"]["temp_wh_sp"],
+                 "temp_in_opt": [h["hvac"]["temp_in_init"]], "temp_wh_opt": [h["wh"]["temp_wh_init"]]}
+            ks = list(keys)
+            if "pv" in h["type"]:
+                ks += ["p_pv_opt", "u_pv_curt_opt"]
+            if "battery" in h["type"]:
+                ks += ["p_batt_ch", "p_batt_disch", "e_batt_opt"]
+                d["e_batt_opt"] = [h["battery"]["e_batt_init"]]
+            for k in ks:
+                d.setdefault(k, [])
+                col = hist[:, L.K[k], i]
+                d[k] += [float(v) for v in col if not np.isnan(v)]
+            out[h["name"]] = d
+        return out
+
+    def summary(self):
+        agg = self.agg_hist[:self.timestep].cpu().numpy()
+        return {"p_grid_aggregate": agg[:, 0].tolist(), "forecast_load": agg[:, 1].tolist(),
+                "agg_cost": agg[:, 2].tolist(), "p_max_aggregate": float(agg[:, 0].max()) if len(agg) else None}

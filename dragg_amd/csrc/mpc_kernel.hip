@@ -46,12 +46,12 @@ struct Lds {
     double *yeq, *zeq, *yeqp, *lam;    // [4H], [4H], [4H], [4(H+1)]
     double *draw, *oat, *ghi, *price;  // [H+1], [H+1], [H+1], [H+1]
     double *sc;                        // [32] scalars
-    int *at, *basic;                   // [8H], [4H]
+    int *at, *basic, *seg;             // [8H], [4H], [12H]
 };
 
 __host__ __device__ inline int lds_doubles(int H) {
     return 64 * H * 2 + 24 * H * 2 + 4 * H + 8 * H * 10 + 4 * H * 3 + 4 * (H + 1) + 4 * (H + 1) + 32 +
-           (8 * H + 4 * H + 1) / 2 + 2;
+           (8 * H + 4 * H + 12 * H + 1) / 2 + 2;
 }
 
 DEV Lds carve(double* s, int H) {
@@ -82,6 +82,7 @@ DEV Lds carve(double* s, int H) {
     L.sc = s; s += 32;
     L.at = reinterpret_cast<int*>(s);
     L.basic = L.at + 8 * H;
+    L.seg = L.basic + 4 * H;
     return L;
 }
 
@@ -379,19 +380,252 @@ DEV double a_times(const Lds& L, const double* xv, int k, int r) {
 }
 
 // --------------------------------------------------------------------------------------
-// exact basis polish: from the ADMM point, pick one basic variable per dynamics row
-// (its own state, or the input that drives it), recompute the vertex by forward
-// substitution, the row duals by backward substitution, and check primal bounds and
-// reduced-cost signs.  On success t1 holds the vertex.
+// exact basis polish.  The LP is three scalar "chains" (indoor T driven by the hvac duty,
+// tank Tw driven by the wh duty and T, battery E driven by charge/discharge):
+//     x_{k+1} = A_k x_k + sum_i B_{k,i} v_{k,i} + C_k ,   boxes on x_{k+1} and v_{k,i}.
+// Given the ADMM active-set guess, a vertex of such a chain is fixed segment by segment:
+// between two states pinned at a bound exactly one input is basic (free), which is solved
+// by a forward sweep from the segment start and a backward sweep from its pinned end.
+// Row duals follow by the mirrored recursion; degenerate segments (no free input) pick,
+// among the locally dual-feasible bases, the one whose first dual is most favourable to
+// the previous pinned state.  Success = every bound and every reduced-cost sign holds,
+// i.e. an exact, certified LP optimum (the vertex a simplex solver would return).
+// Runs on lane 0 (the work is a few sequential passes over the horizon).
 // --------------------------------------------------------------------------------------
-DEV double solve_for(const Lds& L, int k, int r, int bj) {
-    const int o = k * 8;
-    double s = L.beq[k * RS + r];
-    for (int jj = 0; jj < NS; ++jj)
-        if (jj != bj) s -= L.al[k * 24 + r * 8 + jj] * L.t1[o + jj];
-    if (k > 0)
-        for (int jj = 0; jj < NS; ++jj) s -= L.be[k * 24 + r * 8 + jj] * L.t1[o - 8 + jj];
-    return s / L.al[k * 24 + r * 8 + bj];
+struct Chain {
+    int H, sx, ni, sv0, sv1, row;
+    double x0;
+    const double *A, *B, *C, *kap;   // [H], [H][2], [H], [H]   (scratch in L.r)
+    int* seg;                        // [H][4]: start, end, m (-1 tail, -2 degenerate), mi
+    int nseg;
+};
+
+DEV int chain_sv(const Chain& c, int i) { return i == 0 ? c.sv0 : c.sv1; }
+
+DEV double chain_bv(const Chain& c, const Lds& L, int kk) {
+    double bv = 0.0;
+    for (int i = 0; i < c.ni; ++i) bv += c.B[kk * 2 + i] * L.t1[kk * 8 + chain_sv(c, i)];
+    return bv;
+}
+
+// Forward/backward vertex solve of one chain.  The ADMM classification (L.at) is repaired
+// in place where it is inconsistent with a vertex:
+//  * a pinned segment whose forward sweep lands strictly inside the state box -> unpin it;
+//  * a pinned segment that misses its bound -> free the latest input that can close the gap;
+//  * two free inputs in one segment -> pin the state between them closest to its bound.
+DEV bool chain_primal(Chain& c, const Lds& L) {
+    const int H = c.H;
+    double* t1 = L.t1;
+    c.nseg = 0;
+    int start = 0, rescans = 0;
+    double xprev = c.x0;
+    while (start < H) {
+        int j = -1;
+        for (int kk = start; kk < H; ++kk)
+            if (L.at[kk * 8 + c.sx] != 0) { j = kk + 1; break; }
+        const int end = j > 0 ? j : H;
+        int nfree = 0, m = -1, mi = 0, mfirst = -1;
+        for (int kk = start; kk < end; ++kk)
+            for (int i = 0; i < c.ni; ++i)
+                if (L.at[kk * 8 + chain_sv(c, i)] == 0) {
+                    if (mfirst < 0) mfirst = kk;
+                    ++nfree; m = kk; mi = i;
+                }
+        if (j < 0) {                                            // tail: no pinned end
+            if (nfree) return false;
+            double xc = xprev;
+            for (int kk = start; kk < end; ++kk) {
+                xc = c.A[kk] * xc + chain_bv(c, L, kk) + c.C[kk];
+                t1[kk * 8 + c.sx] = xc;
+            }
+            int* sg = c.seg + 4 * c.nseg++;
+            sg[0] = start; sg[1] = end; sg[2] = -1; sg[3] = 0;
+            break;
+        }
+        const int ej = (j - 1) * 8 + c.sx;
+        const double xlo = L.lo[ej], xhi = L.hi[ej];
+        const double xj = (L.at[ej] == -1) ? xlo : xhi;
+        if (nfree > 1) {
+            int bk = -1;
+            double best = 0.0;
+            for (int kk = mfirst; kk < m; ++kk) {
+                const int e = kk * 8 + c.sx;
+                const double span = fmax(L.hi[e] - L.lo[e], 1e-12);
+                const double dist = fmin(fabs(L.x[e] - L.lo[e]), fabs(L.hi[e] - L.x[e])) / span;
+                if (bk < 0 || dist < best) { best = dist; bk = kk; }
+            }
+            if (bk < 0 || rescans > H) return false;
+            const int e = bk * 8 + c.sx;
+            L.at[e] = (fabs(L.x[e] - L.lo[e]) <= fabs(L.hi[e] - L.x[e])) ? -1 : 1;
+            t1[e] = L.at[e] == -1 ? L.lo[e] : L.hi[e];
+            ++rescans;
+            continue;
+        }
+        if (nfree == 0) {                                       // degenerate / misclassified
+            double xc = xprev;
+            for (int kk = start; kk < end; ++kk) {
+                xc = c.A[kk] * xc + chain_bv(c, L, kk) + c.C[kk];
+                t1[kk * 8 + c.sx] = xc;
+            }
+            const bool at_b = fabs(xc - xj) <= TOL_P * (1 + fabs(xj));
+            if (!at_b && xc >= xlo - TOL_P * (1 + fabs(xlo)) && xc <= xhi + TOL_P * (1 + fabs(xhi)) &&
+                rescans <= H) {
+                L.at[ej] = 0;                                   // lands inside the box: not pinned
+                ++rescans;
+                continue;
+            }
+            if (at_b) {
+                t1[ej] = xj;
+                int* sg = c.seg + 4 * c.nseg++;
+                sg[0] = start; sg[1] = end; sg[2] = -2; sg[3] = 0;
+                xprev = xj;
+                start = end;
+                continue;
+            }
+            // misses its bound: free the latest input whose move closes the gap within its box
+            m = -1;
+            double gain = 1.0;
+            for (int kk = end - 1; kk >= start && m < 0; --kk) {
+                for (int i = 0; i < c.ni; ++i) {
+                    const double b = c.B[kk * 2 + i];
+                    if (b == 0.0) continue;
+                    const int ev = kk * 8 + chain_sv(c, i);
+                    const double nv = t1[ev] + (xj - xc) / (b * gain);
+                    if (nv >= L.lo[ev] - TOL_P * (1 + fabs(L.lo[ev])) && nv <= L.hi[ev] + TOL_P * (1 + fabs(L.hi[ev]))) {
+                        m = kk; mi = i;
+                        break;
+                    }
+                }
+                gain *= c.A[kk];
+            }
+            if (m < 0) return false;
+        }
+        // exactly one basic input v_{m,mi}: forward to x_m, backward from the pinned x_j
+        double xc = xprev;
+        for (int kk = start; kk < m; ++kk) {
+            xc = c.A[kk] * xc + chain_bv(c, L, kk) + c.C[kk];
+            t1[kk * 8 + c.sx] = xc;
+        }
+        const double xm = xc;
+        double xn = xj;
+        t1[ej] = xj;
+        for (int kk = end - 1; kk > m; --kk) {
+            xn = (xn - chain_bv(c, L, kk) - c.C[kk]) / c.A[kk];
+            t1[(kk - 1) * 8 + c.sx] = xn;
+        }
+        double rest = 0.0;
+        for (int i = 0; i < c.ni; ++i)
+            if (i != mi) rest += c.B[m * 2 + i] * t1[m * 8 + chain_sv(c, i)];
+        t1[m * 8 + chain_sv(c, mi)] = (xn - c.A[m] * xm - rest - c.C[m]) / c.B[m * 2 + mi];
+        int* sg = c.seg + 4 * c.nseg++;
+        sg[0] = start; sg[1] = end; sg[2] = m; sg[3] = mi;
+        xprev = xj;
+        start = end;
+    }
+    return true;
+}
+
+DEV bool sign_ok(int a, double d, double tol) { return !((a == -1 && d < -tol) || (a == 1 && d > tol)); }
+
+// duals of one segment given its basic choice (cand: -1 = pinned/tail state basic, else
+// k*2+i of the basic input); writes lam[i0..end-1] (lam[end] is known)
+DEV void seg_duals(const Chain& c, const Lds& L, double* lam, int i0, int end, int cand) {
+    auto An = [&](int k) { return k + 1 < c.H ? c.A[k + 1] : 0.0; };
+    if (cand < 0) {
+        for (int k = end - 1; k >= i0; --k) lam[k] = An(k) * lam[k + 1] - L.q[k * 8 + c.sx] - c.kap[k];
+        return;
+    }
+    const int m = cand >> 1, mi = cand & 1;
+    lam[m] = L.q[m * 8 + chain_sv(c, mi)] / c.B[m * 2 + mi];
+    for (int k = m - 1; k >= i0; --k) lam[k] = An(k) * lam[k + 1] - L.q[k * 8 + c.sx] - c.kap[k];
+    for (int k = m; k < end - 1; ++k) lam[k + 1] = (lam[k] + L.q[k * 8 + c.sx] + c.kap[k]) / An(k);
+}
+
+DEV bool chain_dual(const Chain& c, const Lds& L, double* lam /*[H+1]*/, double* trial, double tol) {
+    const int H = c.H;
+    auto An = [&](int k) { return k + 1 < H ? c.A[k + 1] : 0.0; };
+    lam[H] = 0.0;
+    for (int s = c.nseg - 1; s >= 0; --s) {
+        const int* sg = c.seg + 4 * s;
+        const int i0 = sg[0], end = sg[1], m = sg[2], mi = sg[3];
+        if (m >= 0) {
+            seg_duals(c, L, lam, i0, end, m * 2 + mi);
+        } else if (m == -1) {
+            seg_duals(c, L, lam, i0, end, -1);
+        } else {
+            const int side = i0 > 0 ? L.at[(i0 - 1) * 8 + c.sx] : 0;
+            bool found = false;
+            double best = 0.0;
+            for (int cand = -1; cand < 2 * (end - i0); ++cand) {
+                const int cc = cand < 0 ? -1 : ((i0 + (cand >> 1)) * 2 + (cand & 1));
+                if (cand >= 0 && (cand & 1) >= c.ni) continue;
+                for (int k = i0; k <= end; ++k) trial[k] = lam[k];
+                seg_duals(c, L, trial, i0, end, cc);
+                bool fine = true;
+                for (int k = i0; k < end && fine; ++k)
+                    for (int i = 0; i < c.ni; ++i) {
+                        if (cc == k * 2 + i) continue;
+                        const int e = k * 8 + chain_sv(c, i);
+                        if (!sign_ok(L.at[e], L.q[e] - c.B[k * 2 + i] * trial[k], tol)) fine = false;
+                    }
+                if (fine && cc >= 0) {
+                    const int k = end - 1;
+                    const double dx = L.q[k * 8 + c.sx] + c.kap[k] + trial[k] - An(k) * trial[k + 1];
+                    if (!sign_ok(L.at[k * 8 + c.sx], dx, tol)) fine = false;
+                }
+                if (!fine) continue;
+                const double score = trial[i0] * (side == -1 ? 1.0 : (side == 1 ? -1.0 : 0.0));
+                if (!found || score < best) {
+                    found = true;
+                    best = score;
+                    for (int k = i0; k < end; ++k) lam[k] = trial[k];
+                }
+            }
+            if (!found) return false;
+        }
+    }
+    // reduced costs of every nonbasic variable of the chain
+    for (int s = 0; s < c.nseg; ++s) {
+        const int* sg = c.seg + 4 * s;
+        const int i0 = sg[0], end = sg[1], m = sg[2], mi = sg[3];
+        for (int k = i0; k < end; ++k)
+            for (int i = 0; i < c.ni; ++i) {
+                if (m >= 0 && k == m && i == mi) continue;
+                const int e = k * 8 + chain_sv(c, i);
+                if (L.at[e] == 0) return false;
+                if (!sign_ok(L.at[e], L.q[e] - c.B[k * 2 + i] * lam[k], tol)) return false;
+            }
+        if (m >= 0) {
+            const int k = end - 1;
+            const double dx = L.q[k * 8 + c.sx] + c.kap[k] + lam[k] - An(k) * lam[k + 1];
+            if (!sign_ok(L.at[k * 8 + c.sx], dx, tol)) return false;
+        }
+    }
+    return true;
+}
+
+// fill the chain coefficient scratch (L.r: A[H], B[2H], C[H], kap[H]) for chain `which`
+// (0 = indoor T, 1 = tank Tw, 2 = battery E), consistent with build()
+DEV void chain_coefs(const Home& h, const Lds& L, int which, Chain& c, int* seg) {
+    const int H = h.H;
+    double* A = L.r; double* B = L.r + H; double* C = L.r + 3 * H; double* kap = L.r + 4 * H;
+    for (int k = 0; k < H; ++k) {
+        kap[k] = 0.0;
+        if (which == 0) {
+            A[k] = h.aT; B[k * 2] = h.g; B[k * 2 + 1] = 0.0;
+            C[k] = L.oat[k + 1] * h.iR * 3600 * h.inv_c;
+        } else if (which == 1) {
+            const double df = L.draw[k + 1] / h.V, rem = 1 - df, d15 = df * TAP;
+            A[k] = rem + (-rem * h.iRw) * 3600 * h.inv_w; B[k * 2] = h.f; B[k * 2 + 1] = 0.0;
+            C[k] = h.e * L.t1[k * 8 + S_T] + (d15 + ((-d15) * h.iRw) * 3600 * h.inv_w);
+        } else {
+            A[k] = 1.0; B[k * 2] = h.etac / h.dt; B[k * 2 + 1] = (1.0 / h.etad) / h.dt; C[k] = 0.0;
+        }
+    }
+    c.H = H; c.A = A; c.B = B; c.C = C; c.kap = kap; c.seg = seg; c.nseg = 0;
+    if (which == 0) { c.sx = S_T; c.ni = 1; c.sv0 = S_U; c.sv1 = S_U; c.row = 0; c.x0 = h.T0; }
+    else if (which == 1) { c.sx = S_TW; c.ni = 1; c.sv0 = S_W; c.sv1 = S_W; c.row = 1; c.x0 = h.Tw0; }
+    else { c.sx = S_E; c.ni = 2; c.sv0 = S_CH; c.sv1 = S_DIS; c.row = 2; c.x0 = h.E0; }
 }
 
 DEV bool polish(const Home& h, const Lds& L, int lane) {
@@ -408,71 +642,45 @@ DEV bool polish(const Home& h, const Lds& L, int lane) {
         L.at[e] = a;
         L.t1[e] = v;
     }
-    for (int e = lane; e < 4 * (H + 1); e += WAVE) L.lam[e] = 0.0;
-    __syncthreads();
-    if (lane == 0) {
-        int fail = 0;
-        for (int k = 0; k < H && !fail; ++k) {
-            const int o = k * 8;
-            for (int r = 0; r < h.nrows; ++r) {
-                const int own = (r == 0) ? S_T : (r == 1 ? S_TW : S_E);
-                int bj = own;
-                if (L.at[o + own] != 0) {
-                    const int c0 = (r == 0) ? S_U : (r == 1 ? S_W : S_CH);
-                    const int c1 = (r == 2) ? S_DIS : -1;
-                    const bool f0 = L.at[o + c0] == 0, f1 = (c1 >= 0) && L.at[o + c1] == 0;
-                    if (f0 && f1) { fail = 1; break; }
-                    if (f0) bj = c0;
-                    else if (f1) bj = c1;
-                    else {                                  // degenerate: state at bound, try input basic
-                        for (int ci = 0; ci < 2; ++ci) {
-                            const int c = ci == 0 ? c0 : c1;
-                            if (c < 0) continue;
-                            const double v = solve_for(L, k, r, c);
-                            if (v >= L.lo[o + c] - TOL_P * (1 + fabs(L.lo[o + c])) &&
-                                v <= L.hi[o + c] + TOL_P * (1 + fabs(L.hi[o + c]))) { bj = c; break; }
-                        }
-                    }
-                }
-                L.basic[k * RS + r] = bj;
-                L.t1[o + bj] = solve_for(L, k, r, bj);
-            }
-        }
-        if (!fail) {                                        // row duals, backward
-            for (int k = H - 1; k >= 0; --k) {
-                const int o = k * 8;
-                for (int r = h.nrows - 1; r >= 0; --r) {
-                    const int bj = L.basic[k * RS + r];
-                    double s = L.q[o + bj];
-                    for (int r2 = 0; r2 < h.nrows; ++r2) {
-                        if (r2 != r) s += L.al[k * 24 + r2 * 8 + bj] * L.lam[k * RS + r2];
-                        if (k + 1 < H) s += L.be[(k + 1) * 24 + r2 * 8 + bj] * L.lam[(k + 1) * RS + r2];
-                    }
-                    L.lam[k * RS + r] = -s / L.al[k * 24 + r * 8 + bj];
-                }
-            }
-        }
-        L.sc[0] = fail;
-    }
-    __syncthreads();
-    if (L.sc[0] != 0.0) return false;
     double qmax = 0.0;
     for (int e = lane; e < n; e += WAVE) qmax = fmax(qmax, fabs(L.q[e]));
     qmax = wave_max(qmax);
+    __syncthreads();
+    if (lane == 0) {
+        bool ok = true;
+        double* mu = L.zeq;                 // [H+1] tank duals (zeq is scratch here)
+        double* trial = L.t2;               // [H+1]
+        Chain cT, cW, cE;
+        // primal: T, then Tw (its C depends on T)
+        chain_coefs(h, L, 0, cT, L.seg);
+        ok = chain_primal(cT, L);
+        if (ok) { chain_coefs(h, L, 1, cW, L.seg + 4 * H); ok = chain_primal(cW, L); }
+        // duals: Tw first (mu), then T with the coupling kap_k = -e mu_k (T_{k+1} sits in row W_k)
+        const double tol = TOL_D * (qmax + 1e-30);
+        if (ok) ok = chain_dual(cW, L, mu, trial, tol);
+        if (ok) {
+            const int nsegT = cT.nseg;            // chain_coefs refills the scratch and resets nseg
+            chain_coefs(h, L, 0, cT, L.seg);
+            cT.nseg = nsegT;
+            double* kap = L.r + 4 * H;
+            for (int k = 0; k < H; ++k) kap[k] = -h.e * mu[k];
+            double* lam = L.t2 + (H + 1);   // t2 holds 8H >= 2(H+1)
+            ok = chain_dual(cT, L, lam, trial, tol);
+        }
+        if (ok && h.batt) {
+            chain_coefs(h, L, 2, cE, L.seg + 8 * H);
+            ok = chain_primal(cE, L);
+            if (ok) ok = chain_dual(cE, L, L.t2 + 2 * (H + 1), trial, tol);
+        }
+        L.sc[0] = ok ? 0.0 : 1.0;
+    }
+    __syncthreads();
+    if (L.sc[0] != 0.0) return false;
     bool bad = false;
     for (int e = lane; e < n; e += WAVE) {
-        const int k = e >> 3, jj = e & 7;
-        const int a = L.at[e];
-        if (a == 2) continue;
+        if (L.at[e] == 2) continue;
         const double v = L.t1[e];
-        if (v < L.lo[e] - TOL_P * (1 + fabs(L.lo[e])) || v > L.hi[e] + TOL_P * (1 + fabs(L.hi[e]))) bad = true;
-        bool isb = false;
-        for (int r = 0; r < h.nrows; ++r) isb |= (L.basic[k * RS + r] == jj);
-        if (isb) continue;
-        if (a == 0) { bad = true; continue; }
-        const double d = L.q[e] + at_times(h, L, L.lam, k, jj);
-        const double tol = TOL_D * qmax + 1e-14;
-        if ((a == -1 && d < -tol) || (a == 1 && d > tol)) bad = true;
+        if (!(v >= L.lo[e] - TOL_P * (1 + fabs(L.lo[e])) && v <= L.hi[e] + TOL_P * (1 + fabs(L.hi[e])))) bad = true;
     }
     return !wave_any(bad);
 }
@@ -727,6 +935,7 @@ DEV void write_success(const Home& h, const Lds& L, const Io& io, int lane) {
 // failure branch (mpc_calc.py:527-595); returns dragg_status (ERR_PARSE where the
 // reference would raise)
 DEV int write_fallback(const Home& h, const Lds& L, const Io& io, int status) {
+#pragma clang fp contract(off)   // bit-identical to the reference's float expressions
     const int H = h.H;
     const double S = h.S;
     int counter = h.counter + 1;
@@ -825,6 +1034,7 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
         }
         __syncthreads();
     } else {
+#pragma clang fp contract(off)   // draw sizes, Tw0 mixing and the season test as in numpy
         const int t = a.t;
         h.t = t;
         const int dt = h.dt;
@@ -855,7 +1065,7 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
             if (a.noise) z = a.noise[(size_t)k * N + home];
             else {
                 double z0, z1;
-                normal_pair(a.p.seed, home, t, k >> 1, &z0, &z1);
+                normal_pair(a.p.seed, a.p.home_offset + home, t, k >> 1, &z0, &z1);
                 z = (k & 1) ? z1 : z0;
             }
             mx = fmax(mx, a.p.oat[s0 + k + 1] + pow(1.1, (double)k) * z);
@@ -954,13 +1164,13 @@ __global__ __launch_bounds__(256) void aggregate_kernel(const double* vals, int 
     if (threadIdx.x < 3) out3[threadIdx.x] = red[threadIdx.x][0];
 }
 
-__global__ void noise_kernel(int N, int H, uint64_t seed, int t, double* out) {
+__global__ void noise_kernel(int N, int H, uint64_t seed, int off, int t, double* out) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const int pairs = (H + 1) / 2;
     if (idx >= N * pairs) return;
     const int home = idx % N, pr = idx / N;
     double z0, z1;
-    normal_pair(seed, home, t, pr, &z0, &z1);
+    normal_pair(seed, off + home, t, pr, &z0, &z1);
     out[(size_t)(2 * pr) * N + home] = z0;
     if (2 * pr + 1 < H) out[(size_t)(2 * pr + 1) * N + home] = z1;
 }
@@ -1048,13 +1258,13 @@ int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, 
     return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
 }
 
-int dragg_mpc_season_noise(const dragg_mpc_dims* dims, uint64_t seed, int32_t timestep, double* noise_out,
-                           void* stream) {
+int dragg_mpc_season_noise(const dragg_mpc_dims* dims, uint64_t seed, int32_t home_offset, int32_t timestep,
+                           double* noise_out, void* stream) {
     if (!dims || !noise_out || dims->n_homes < 0 || dims->horizon < 1) return DRAGG_E_ARG;
     const int total = dims->n_homes * ((dims->horizon + 1) / 2);
     if (total == 0) return DRAGG_OK;
     hipLaunchKernelGGL(noise_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                       dims->n_homes, dims->horizon, seed, timestep, noise_out);
+                       dims->n_homes, dims->horizon, seed, home_offset, timestep, noise_out);
     return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
 }
 

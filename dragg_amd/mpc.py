@@ -96,7 +96,7 @@ class MPCBatch:
     """
 
     def __init__(self, homes, oat=None, ghi=None, tou=None, start_index=0, reward_price=(0.0,),
-                 int_mode="round", seed=0, max_iter=4000, check_every=10, device="cuda"):
+                 int_mode="round", seed=0, max_iter=4000, check_every=10, device="cuda", home_offset=0):
         self.lib = L.load()
         if not torch.cuda.is_available():
             raise L.DraggError("no GPU visible: the batched MPC has no CPU fallback")
@@ -115,6 +115,7 @@ class MPCBatch:
                            int_mode=L.INT_ROUND if int_mode == "round" else L.INT_RELAX,
                            max_iter=max_iter, check_every=check_every, discount=dm["discount"])
         self.seed = int(seed)
+        self.home_offset = int(home_offset)
         self.set_environment(oat if oat is not None else [0.0], ghi if ghi is not None else [0.0],
                              tou if tou is not None else [0.0], start_index)
         self.set_reward_price(reward_price)
@@ -152,7 +153,8 @@ class MPCBatch:
     def _problem(self):
         return L.Problem(params=L.ptr(self.params), home_type=L.ptr(self.types), draw_hourly=L.ptr(self.draws),
                          oat=L.ptr(self.oat), ghi=L.ptr(self.ghi), tou=L.ptr(self.tou),
-                         reward_price=L.ptr(self.rp), start_index=self.start_index, seed=self.seed)
+                         reward_price=L.ptr(self.rp), start_index=self.start_index,
+                         home_offset=self.home_offset, seed=self.seed)
 
     def _hash(self):
         return L.Hash(vals=L.ptr(self.vals), fc=L.ptr(self.fc))
@@ -203,7 +205,7 @@ class MPCBatch:
 
     def season_noise(self, t, stream=None):
         out = torch.empty((self.H, self.N), dtype=torch.float64, device=self.device)
-        L.check(self.lib.dragg_mpc_season_noise(ctypes.byref(self.dims), self.seed, int(t), L.ptr(out),
+        L.check(self.lib.dragg_mpc_season_noise(ctypes.byref(self.dims), self.seed, self.home_offset, int(t), L.ptr(out),
                                                 L.stream_ptr(stream)))
         return out
 

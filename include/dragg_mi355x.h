@@ -128,7 +128,7 @@ typedef struct dragg_mpc_problem {
     const double* tou;          /* [n_env] redis 'tou' list                             */
     const double* reward_price; /* [n_rp]  redis 'reward_price' list                    */
     int32_t start_index;        /* start_hour_index (aggregator.py:630-638)             */
-    int32_t _pad;
+    int32_t home_offset;        /* global index of home 0 of this shard (noise key)     */
     uint64_t seed;              /* keyed season-noise stream when noise == NULL         */
 } dragg_mpc_problem;
 
@@ -187,8 +187,8 @@ int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, 
 
 /* The keyed season-noise stream used when noise == NULL: writes [H][N] normals for
    timestep t (exposed so the host and tests can reproduce the draw). */
-int dragg_mpc_season_noise(const dragg_mpc_dims* dims, uint64_t seed, int32_t timestep,
-                           double* noise_out, void* stream);
+int dragg_mpc_season_noise(const dragg_mpc_dims* dims, uint64_t seed, int32_t home_offset,
+                           int32_t timestep, double* noise_out, void* stream);
 
 #ifdef __cplusplus
 }

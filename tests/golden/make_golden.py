@@ -45,8 +45,12 @@ SCENARIOS = {
     "c3_h48": dict(n=6, batt=0, pv=2, pvb=0, start="2015-01-01 00", end="2015-01-01 04",
                    dt=4, horizon=12, action_horizon=12, seed=7, record_t=range(0, 16)),
     # hourly steps (dt=1), different season/time of year: exercises summer mode and tou.
-    "summer_dt1": dict(n=8, batt=2, pv=2, pvb=2, start="2015-07-10 00", end="2015-07-11 00",
+    "summer_dt1": dict(n=6, batt=0, pv=3, pvb=0, start="2015-07-10 00", end="2015-07-11 00",
                        dt=1, horizon=6, action_horizon=6, seed=3, record_t=range(0, 24)),
+    # spring, hourly steps, all four types (battery homes must not fail at t=0: the reference
+    # then raises KeyError('e_batt_opt') at t=1, mpc_calc.py:285)
+    "spring_dt1": dict(n=8, batt=2, pv=2, pvb=2, start="2015-04-02 00", end="2015-04-03 00",
+                       dt=1, horizon=4, action_horizon=4, seed=5, record_t=range(0, 24)),
 }
 
 CONFIG_TMPL = """
