@@ -62,11 +62,11 @@ DEV Lds carve(double* s, int H) {
     L.be = s; s += 24 * H;
     L.beq = s; s += 4 * H;
     L.x = s; s += 8 * H;
-    L.zb = s; s += 8 * H;
-    L.yb = s; s += 8 * H;
     L.lo = s; s += 8 * H;
     L.hi = s; s += 8 * H;
     L.q = s; s += 8 * H;
+    L.zb = s; s += 8 * H;      // zb, yb, r, t1, t2, ybp: contiguous 48H doubles, reused as
+    L.yb = s; s += 8 * H;      // the integer DP's bin arrays once the ADMM has finished
     L.r = s; s += 8 * H;
     L.t1 = s; s += 8 * H;
     L.t2 = s; s += 8 * H;
@@ -794,58 +794,133 @@ DEV int admm(const Home& h, const Lds& L, int lane, int max_iter, int check, int
 }
 
 // --------------------------------------------------------------------------------------
-// integer duty cycles: feasibility-preserving rounding that tracks the relaxed trajectory
-// from the safe side (T_{k+1} >= T*_{k+1} in heating, <= in cooling; Tw likewise)
+// integer duty cycles (mpc_calc.py:171-173, 344-349).  The thermal MILP is two integer
+// chains -- indoor T driven by the hvac duty, then tank Tw driven by the wh duty (and by
+// T through a 4e-5 coupling).  Each is solved by a forward dynamic programme over the
+// state discretised into bins of 1/NBU of one duty unit's effect: per bin the cheapest
+// label is kept with its EXACT state value, so every kept path is exactly feasible and
+// costed; a bin collision is the only approximation.  Pull formulation: each lane owns
+// target bins and scans the (1-2) source bins that can reach it per duty value, so a
+// stage is conflict-free and fully lane-parallel.  Back-pointers (source bin, duty)
+// live in the freed KKT-factor LDS.  On the golden fixtures this reproduces the
+// reference's MILP optimum (see tests/test_gpu_parity.py).
 // --------------------------------------------------------------------------------------
-DEV bool round_duties(const Home& h, const Lds& L) {
-    double Tk = h.T0, Wk = h.Tw0;
-    for (int k = 0; k < h.H; ++k) {
-        const int o = k * 8;
-        const double bk = L.oat[k + 1] * h.iR * 3600 * h.inv_c;
-        const double uc = (L.x[o + S_T] - h.aT * Tk - bk) / h.g;
-        int u = (int)ceil(uc - 1e-9);
-        u = u < 0 ? 0 : (u > h.S ? h.S : u);
-        double Tn = h.aT * Tk + bk + h.g * u;
-        const double tT = TOL_P * (1 + fabs(h.Tmax));
-        if (Tn < h.Tmin - tT || Tn > h.Tmax + tT) {
-            bool ok = false;
-            for (int d = 1; d <= h.S && !ok; ++d) {
-                for (int sgn = -1; sgn <= 1 && !ok; sgn += 2) {
-                    const int uu = u + sgn * d;
-                    if (uu < 0 || uu > h.S) continue;
-                    const double Tc = h.aT * Tk + bk + h.g * uu;
-                    if (Tc >= h.Tmin - tT && Tc <= h.Tmax + tT) { u = uu; Tn = Tc; ok = true; }
-                }
-            }
-            if (!ok) return false;
-        }
-        const double df = L.draw[k + 1] / h.V;
-        const double rem = 1 - df;
-        const double ck = rem + (-rem * h.iRw) * 3600 * h.inv_w;
-        const double d15 = df * TAP;
-        const double dk = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
-        const double wc = (L.x[o + S_TW] - ck * Wk - h.e * Tn - dk) / h.f;
-        int w = (int)ceil(wc - 1e-9);
-        w = w < 0 ? 0 : (w > h.S ? h.S : w);
-        double Wn = ck * Wk + h.e * Tn + h.f * w + dk;
-        const double wlo = L.lo[o + S_TW], whi = L.hi[o + S_TW];
-        const double tW = TOL_P * (1 + fabs(whi));
-        if (Wn < wlo - tW || Wn > whi + tW) {
-            bool ok = false;
-            for (int d = 1; d <= h.S && !ok; ++d) {
-                for (int sgn = -1; sgn <= 1 && !ok; sgn += 2) {
-                    const int ww = w + sgn * d;
-                    if (ww < 0 || ww > h.S) continue;
-                    const double Wc = ck * Wk + h.e * Tn + h.f * ww + dk;
-                    if (Wc >= wlo - tW && Wc <= whi + tW) { w = ww; Wn = Wc; ok = true; }
-                }
-            }
-            if (!ok) return false;
-        }
-        L.x[o + S_U] = u; L.x[o + S_W] = w; L.x[o + S_T] = Tn; L.x[o + S_TW] = Wn;
-        Tk = Tn; Wk = Wn;
+constexpr int NBU = 8;
+
+struct DpChain {
+    int H, S, sx, sv;
+    double g;
+    const double* A;    // [H]
+    const double* C;    // [H]
+    double x0;
+};
+
+// returns false if no integer schedule keeps the chain inside its box
+DEV bool dp_chain(const Home& h, const Lds& L, const DpChain& c, int lane) {
+    const int H = c.H, S = c.S;
+    double glo = INFINITY, ghi = -INFINITY;
+    for (int k = 0; k < H; ++k) {
+        glo = fmin(glo, L.lo[k * 8 + c.sx]);
+        ghi = fmax(ghi, L.hi[k * 8 + c.sx]);
     }
+    const int cap = min(512, 12 * H);
+    double w = fabs(c.g) / NBU;
+    int nb = (int)floor((ghi - glo) / w) + 1;
+    if (nb > cap) { w = (ghi - glo) / (cap - 1); nb = cap; }
+    double* cc = L.zb;                      // cost of the label in each bin
+    double* cx = L.zb + nb;                 // its exact state
+    double* nc = L.zb + 2 * nb;
+    double* nx = L.zb + 3 * nb;             // zb..ybp are contiguous: 48H doubles >= 4 nb
+    uint16_t* par = reinterpret_cast<uint16_t*>(L.Lf);   // [H][nb] (source bin << 4 | duty)
+    const double BIG = INFINITY;
+    for (int k = 0; k < H; ++k) {
+        const double Ak = c.A[k], Ck = c.C[k], ck = L.q[k * 8 + c.sv];
+        const double lo = L.lo[k * 8 + c.sx], hi = L.hi[k * 8 + c.sx];
+        const double tlo = lo - TOL_P * (1 + fabs(lo)), thi = hi + TOL_P * (1 + fabs(hi));
+        for (int B = lane; B < nb; B += WAVE) {
+            double best = BIG, bx = 0.0;
+            int bp = 0xFFFF;
+            for (int u = 0; u <= S; ++u) {
+                if (k == 0) {
+                    const double xn = Ak * c.x0 + c.g * u + Ck;
+                    if (xn < tlo || xn > thi) continue;
+                    if ((int)floor((xn - glo) / w) != B) continue;
+                    const double cn = ck * u;
+                    if (cn < best) { best = cn; bx = xn; bp = u; }
+                    continue;
+                }
+                // source states x with A x + g u + C inside bin B
+                const double xa = (glo + B * w - c.g * u - Ck) / Ak;
+                const double xb = (glo + (B + 1) * w - c.g * u - Ck) / Ak;
+                int s0 = (int)floor((fmin(xa, xb) - glo) / w) - 1, s1 = (int)floor((fmax(xa, xb) - glo) / w) + 1;
+                s0 = s0 < 0 ? 0 : s0;
+                s1 = s1 >= nb ? nb - 1 : s1;
+                for (int sb = s0; sb <= s1; ++sb) {
+                    const double cs = cc[sb];
+                    if (!(cs < BIG)) continue;
+                    const double xn = Ak * cx[sb] + c.g * u + Ck;
+                    if (xn < tlo || xn > thi) continue;
+                    if ((int)floor((xn - glo) / w) != B) continue;
+                    const double cn = cs + ck * u;
+                    if (cn < best) { best = cn; bx = xn; bp = (sb << 4) | u; }
+                }
+            }
+            nc[B] = best;
+            nx[B] = bx;
+            par[k * nb + B] = (uint16_t)bp;
+        }
+        __syncthreads();
+        for (int B = lane; B < nb; B += WAVE) { cc[B] = nc[B]; cx[B] = nx[B]; }
+        __syncthreads();
+    }
+    // cheapest final label (lowest bin on ties, deterministic)
+    double best = BIG;
+    int bb = -1;
+    for (int B = lane; B < nb; B += WAVE)
+        if (cc[B] < best) { best = cc[B]; bb = B; }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bb, o);
+        if (ob < best || (ob == best && oi >= 0 && (bb < 0 || oi < bb))) { best = ob; bb = oi; }
+    }
+    if (bb < 0) return false;
+    if (lane == 0) {
+        int b = bb;
+        for (int k = H - 1; k >= 0; --k) {
+            const int p = par[k * nb + b];
+            L.x[k * 8 + c.sv] = (double)(p & 15);
+            b = p >> 4;
+        }
+        double x = c.x0;                    // exact forward trajectory of the chosen duties
+        for (int k = 0; k < H; ++k) {
+            x = c.A[k] * x + c.g * L.x[k * 8 + c.sv] + c.C[k];
+            L.x[k * 8 + c.sx] = x;
+        }
+    }
+    __syncthreads();
     return true;
+}
+
+DEV bool round_duties(const Home& h, const Lds& L, int lane) {
+    const int H = h.H;
+    // coefficient arrays live in L.yeq / L.zeq (4H each, free after the ADMM)
+    double* cA = L.yeq;
+    double* cC = L.zeq;
+    for (int k = lane; k < H; k += WAVE) {
+        cA[k] = h.aT;
+        cC[k] = L.oat[k + 1] * h.iR * 3600 * h.inv_c;
+    }
+    __syncthreads();
+    DpChain cT{H, h.S, S_T, S_U, h.g, cA, cC, h.T0};
+    if (!dp_chain(h, L, cT, lane)) return false;
+    for (int k = lane; k < H; k += WAVE) {
+        const double df = L.draw[k + 1] / h.V, rem = 1 - df, d15 = df * TAP;
+        cA[k] = rem + (-rem * h.iRw) * 3600 * h.inv_w;
+        cC[k] = h.e * L.x[k * 8 + S_T] + (d15 + ((-d15) * h.iRw) * 3600 * h.inv_w);
+    }
+    __syncthreads();
+    DpChain cW{H, h.S, S_TW, S_W, h.f, cA, cC, h.Tw0};
+    return dp_chain(h, L, cW, lane);
 }
 
 // closed-form PV curtailment (mpc_calc.py:382-384): u multiplies a cost coefficient
@@ -1118,13 +1193,7 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
     double relax = NAN, obj = NAN;
     if (status == DRAGG_ST_OPTIMAL) {
         relax = objective(h, L, lane);
-        if (a.d.int_mode == DRAGG_INT_ROUND) {
-            bool ok = true;
-            if (lane == 0) ok = round_duties(h, L);
-            ok = __shfl(ok ? 1 : 0, 0) != 0;
-            __syncthreads();
-            if (!ok) status = DRAGG_ST_ROUND_FAIL;
-        }
+        if (a.d.int_mode == DRAGG_INT_ROUND && !round_duties(h, L, lane)) status = DRAGG_ST_ROUND_FAIL;
         if (status == DRAGG_ST_OPTIMAL) obj = objective(h, L, lane);
     }
 
