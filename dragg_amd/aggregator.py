@@ -29,14 +29,16 @@ def shard_bounds(n, rank, world):
 class DeviceAggregator:
     def __init__(self, homes, oat, ghi, tou, start_index=0, num_timesteps=96, reward_price=(0.0,),
                  int_mode="round", seed=0, rank=0, world=1, group=None, keep_history=True,
-                 max_iter=4000, check_every=10, device=None):
+                 max_iter=4000, check_every=10, device=None, batch_cls=MPCBatch):
         self.rank, self.world, self.group = rank, world, group
         lo, hi = shard_bounds(len(homes), rank, world)
         self.lo, self.hi = lo, hi
         self.all_homes = homes
         self.homes = homes[lo:hi]
         dev = device or torch.device("cuda", torch.cuda.current_device())
-        self.batch = MPCBatch(self.homes, oat, ghi, tou, start_index, reward_price, int_mode=int_mode,
+        # batch_cls is injectable only so the multi-rank glue can be exercised with gloo on
+        # CPU (tests/test_distributed.py); the solver itself is MPCBatch (HIP, no fallback).
+        self.batch = batch_cls(self.homes, oat, ghi, tou, start_index, reward_price, int_mode=int_mode,
                               seed=seed, home_offset=lo, max_iter=max_iter, check_every=check_every,
                               device=dev)
         self.num_timesteps = num_timesteps

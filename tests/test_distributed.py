@@ -1,0 +1,90 @@
+"""Multi-rank glue of the device-resident driver on CPU with gloo (world size 2).
+
+The solver is replaced by a stand-in batch (the HIP solver needs a GPU); what is tested is
+the sharding (contiguous blocks of the global community order, keyed by the global index)
+and the per-step all-reduce of [agg_load, forecast_load, agg_cost] (aggregator.py:751-753).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dragg_amd.aggregator import DeviceAggregator, shard_bounds
+
+
+class FakeBatch:
+    """Deterministic stand-in: each home contributes (index+1)*t to the three sums."""
+
+    def __init__(self, homes, *a, home_offset=0, device=None, **kw):
+        self.N, self.H = len(homes), 4
+        self.off = home_offset
+        self.t = 0
+        self.status = torch.zeros(self.N, dtype=torch.int32)
+        self.iters = torch.zeros(self.N, dtype=torch.int32)
+        self.types_host = None
+
+    def step(self, t, noise=None, hist=None):
+        self.t = t
+        if hist is not None:
+            hist.zero_()
+            hist[0] = torch.arange(self.off, self.off + self.N, dtype=torch.float64)
+
+    def aggregate(self):
+        idx = torch.arange(self.off, self.off + self.N, dtype=torch.float64) + 1
+        s = float(idx.sum()) * self.t
+        return torch.tensor([s, 2 * s, 3 * s], dtype=torch.float64)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, steps, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    homes = [{"name": f"h{i}"} for i in range(n)]
+    agg = DeviceAggregator(homes, None, None, None, 0, steps, rank=rank, world=world,
+                           device=torch.device("cpu"), batch_cls=FakeBatch)
+    out = [agg.collect_data().tolist() for _ in range(0)]
+    for _ in range(steps):
+        agg.run_iteration()
+        out.append(agg.collect_data().tolist())
+    q.put((rank, agg.lo, agg.hi, out, agg.hist[:, 0, :].tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [7, 10])
+def test_two_rank_allreduce_and_sharding(n):
+    world, steps = 2, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    # contiguous, disjoint, covering shards
+    assert res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == n
+    total = sum(range(1, n + 1))
+    for rank, lo, hi, out, hist in res:
+        for t, v in enumerate(out):
+            assert v == [total * t, 2 * total * t, 3 * total * t]      # all-reduced sums, every rank
+        assert hist[0] == list(map(float, range(lo, hi)))              # global home indices
+
+
+def test_shard_bounds_cover():
+    for n in range(0, 40):
+        for w in (1, 2, 3, 8):
+            parts = [shard_bounds(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
