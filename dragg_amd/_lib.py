@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libdragg_mi355x.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # enums (mirror include/dragg_mi355x.h)
 BASE, PV_ONLY, BATTERY_ONLY, PV_BATTERY = 0, 1, 2, 3
@@ -35,6 +35,9 @@ STATUS_NAMES = ["optimal", "infeasible", "infeasible_cert", "max_iter", "round_f
 
 INT_ROUND, INT_RELAX = 0, 1
 
+PHASES = ["setup", "iter", "factor", "polish", "check", "integer", "write"]
+NPHASE = len(PHASES)
+
 c_dp = ctypes.c_void_p  # device pointers are passed as raw integers
 
 
@@ -56,7 +59,8 @@ class Hash(ctypes.Structure):
 
 
 class Out(ctypes.Structure):
-    _fields_ = [("status", c_dp), ("iters", c_dp), ("obj", c_dp), ("relax_obj", c_dp), ("hist", c_dp)]
+    _fields_ = [("status", c_dp), ("iters", c_dp), ("obj", c_dp), ("relax_obj", c_dp), ("hist", c_dp),
+                ("cycles", c_dp)]
 
 
 class Explicit(ctypes.Structure):

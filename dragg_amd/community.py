@@ -27,7 +27,13 @@ CONFIG_RANGES = dict(  # config.toml:32-58
 )
 
 
-def half_hourly_weather(days, seed=0, t_mean=10.0, t_amp=5.0, ghi_peak=323.0):
+# Houston-like monthly climate (NSRDB-shaped): mean OAT, diurnal amplitude, clear-sky GHI peak,
+# daylight window.  January matches dragg/data/nsrdb.csv's first days (OAT 5-15 C, peak ~323).
+CLIMATE = {1: (10.0, 5.0, 323.0, 7.0, 17.5), 4: (21.0, 5.0, 760.0, 6.5, 19.0),
+           7: (29.0, 5.0, 900.0, 6.0, 20.0), 10: (22.0, 5.0, 650.0, 7.0, 18.5)}
+
+
+def half_hourly_weather(days, seed=0, t_mean=10.0, t_amp=5.0, ghi_peak=323.0, sun=(7.0, 17.5)):
     """Integer OAT (C) and GHI (W/m2) at :00 and :30 of each hour (NSRDB rows)."""
     rng = np.random.default_rng(seed)
     n = days * 48
@@ -38,7 +44,9 @@ def half_hourly_weather(days, seed=0, t_mean=10.0, t_amp=5.0, ghi_peak=323.0):
     oat = t_mean + drift + t_amp * np.sin(2 * math.pi * (hod - 9) / 24) + rng.normal(0, 0.4, n)
     oat = np.trunc(oat).astype(int)
     cloud = np.repeat(rng.uniform(0.55, 1.0, days + 1), 48)[:n]
-    ghi = np.where((hod >= 7) & (hod <= 17.5), ghi_peak * cloud * np.sin(math.pi * (hod - 7) / 10.5), 0.0)
+    rise, set_ = sun
+    ghi = np.where((hod >= rise) & (hod <= set_),
+                   ghi_peak * cloud * np.sin(math.pi * (hod - rise) / (set_ - rise)), 0.0)
     ghi = np.trunc(np.clip(ghi, 0, None)).astype(int)
     del day
     return oat, ghi
@@ -57,10 +65,11 @@ def tou_hourly(hours, start_hour=0, base=0.07, shoulder=(9, 21), shoulder_price=
     return np.where((hod >= shoulder[0]) & (hod < shoulder[1]), shoulder_price, base)
 
 
-def synthetic_weather(days, dt, sim_hours, seed=0):
+def synthetic_weather(days, dt, sim_hours, seed=0, month=1):
     """(oat, ghi, tou) lists at dt steps per hour covering `days` days; tou forward-filled past
-    `sim_hours` like `join_data` (aggregator.py:219-230)."""
-    oat_hh, ghi_hh = half_hourly_weather(days, seed)
+    `sim_hours` like `join_data` (aggregator.py:219-230).  `month` picks the climate row."""
+    tm, ta, gp, rise, set_ = CLIMATE[month]
+    oat_hh, ghi_hh = half_hourly_weather(days, seed, tm, ta, gp, (rise, set_))
     oat = upsample(oat_hh, dt).astype(float)
     ghi = upsample(ghi_hh, dt).astype(float)
     tou_h = tou_hourly(sim_hours)

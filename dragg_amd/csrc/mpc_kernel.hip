@@ -105,6 +105,24 @@ DEV double wave_sum(double v) {
 }
 DEV bool wave_any(bool p) { return __any(p); }
 
+// per-phase shader-cycle stamps (dragg_mpc_out.cycles; diagnostic, off when NULL)
+struct Prof {
+    unsigned long long acc[DRAGG_NPHASE];
+    unsigned long long t;
+    bool on;
+    __device__ __forceinline__ void start(bool enable) {
+        on = enable;
+        for (int i = 0; i < DRAGG_NPHASE; ++i) acc[i] = 0;
+        t = on ? __builtin_amdgcn_s_memtime() : 0;
+    }
+    __device__ __forceinline__ void mark(int phase) {
+        if (!on) return;
+        const unsigned long long n = __builtin_amdgcn_s_memtime();
+        acc[phase] += n - t;
+        t = n;
+    }
+};
+
 // --------------------------------------------------------------------------------------
 // keyed season noise: Philox4x32-10 + Box-Muller (replaces the worker-global
 // np.random.randn of mpc_calc.py:222, which is not reproducible across runs)
@@ -689,7 +707,7 @@ DEV bool polish(const Home& h, const Lds& L, int lane) {
 // OSQP-style ADMM on  min q'x  s.t.  A_eq x = b,  lo <= x <= hi
 // returns dragg_status; on DRAGG_ST_OPTIMAL, L.x holds the exact vertex
 // --------------------------------------------------------------------------------------
-DEV int admm(const Home& h, const Lds& L, int lane, int max_iter, int check, int* iters) {
+DEV int admm(const Home& h, const Lds& L, int lane, int max_iter, int check, int* iters, Prof& pf) {
     const int H = h.H, n = NS * H, m = RS * H;
     double rho = RHO0;
     for (int e = lane; e < n; e += WAVE) {
@@ -698,7 +716,9 @@ DEV int admm(const Home& h, const Lds& L, int lane, int max_iter, int check, int
     }
     for (int e = lane; e < m; e += WAVE) { L.yeq[e] = 0.0; L.yeqp[e] = 0.0; }
     __syncthreads();
+    pf.mark(DRAGG_PH_ITER);
     factor(h, L, lane, rho);
+    pf.mark(DRAGG_PH_FACTOR);
     for (int it = 1; it <= max_iter; ++it) {
         const double rq = RHO_EQ * rho;
         // rhs = sigma x - q + A_eq'(rq b - y_eq) + (rho z_b - y_b)
@@ -734,7 +754,10 @@ DEV int admm(const Home& h, const Lds& L, int lane, int max_iter, int check, int
         }
         __syncthreads();
         if (it % check != 0) continue;
-        if (polish(h, L, lane)) {
+        pf.mark(DRAGG_PH_ITER);
+        const bool pol = polish(h, L, lane);
+        pf.mark(DRAGG_PH_POLISH);
+        if (pol) {
             for (int e = lane; e < n; e += WAVE) L.x[e] = L.t1[e];
             __syncthreads();
             *iters = it;
@@ -784,9 +807,11 @@ DEV int admm(const Home& h, const Lds& L, int lane, int max_iter, int check, int
         const double sd = rd / fmax(fmax(naty, nq), 1e-12);
         double nr = rho * sqrt(sp / fmax(sd, 1e-12));
         nr = fmin(fmax(nr, 1e-6), 1e6);
+        pf.mark(DRAGG_PH_CHECK);
         if (nr > 5.0 * rho || nr < 0.2 * rho) {
             rho = nr;
             factor(h, L, lane, rho);
+            pf.mark(DRAGG_PH_FACTOR);
         }
     }
     *iters = max_iter;
@@ -1094,6 +1119,8 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
     Lds L = carve(smem, H);
     Io io{a.vals, a.fc, N, home};
     int status_pre = -1;
+    Prof pf;
+    pf.start(a.out.cycles != nullptr);
 
     // ---------------- inputs (get_initial_conditions / set_environmental_variables)
     if (EXPLICIT) {
@@ -1188,12 +1215,16 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
     else {
         const int mi = a.d.max_iter > 0 ? a.d.max_iter : 4000;
         const int ce = a.d.check_every > 0 ? a.d.check_every : 10;
-        status = admm(h, L, lane, mi, ce, &iters);
+        pf.mark(DRAGG_PH_SETUP);
+        status = admm(h, L, lane, mi, ce, &iters, pf);
     }
+    pf.mark(DRAGG_PH_SETUP);
     double relax = NAN, obj = NAN;
     if (status == DRAGG_ST_OPTIMAL) {
         relax = objective(h, L, lane);
+        pf.mark(DRAGG_PH_WRITE);
         if (a.d.int_mode == DRAGG_INT_ROUND && !round_duties(h, L, lane)) status = DRAGG_ST_ROUND_FAIL;
+        pf.mark(DRAGG_PH_INTEGER);
         if (status == DRAGG_ST_OPTIMAL) obj = objective(h, L, lane);
     }
 
@@ -1212,6 +1243,9 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
     }
     if (a.out.hist && lane == 0)      // lane 0 wrote every vals field of this home
         for (int k = 0; k < DRAGG_NVAL; ++k) a.out.hist[(size_t)k * N + home] = io.v(k);
+    pf.mark(DRAGG_PH_WRITE);
+    if (pf.on && lane == 0)
+        for (int k = 0; k < DRAGG_NPHASE; ++k) a.out.cycles[(size_t)k * N + home] = (int64_t)pf.acc[k];
 }
 
 __global__ __launch_bounds__(256) void aggregate_kernel(const double* vals, int N, double* out3) {

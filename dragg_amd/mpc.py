@@ -126,6 +126,7 @@ class MPCBatch:
         self.obj = torch.zeros(self.N, dtype=torch.float64, device=dev)
         self.relax_obj = torch.zeros(self.N, dtype=torch.float64, device=dev)
         self.agg = torch.zeros(3, dtype=torch.float64, device=dev)
+        self.cycles = None
         rc = self.lib.dragg_mpc_lds_bytes(ctypes.byref(self.dims))
         if rc < 0:
             L.check(rc)
@@ -161,7 +162,11 @@ class MPCBatch:
 
     def _out(self, hist=None):
         return L.Out(status=L.ptr(self.status), iters=L.ptr(self.iters), obj=L.ptr(self.obj),
-                     relax_obj=L.ptr(self.relax_obj), hist=L.ptr(hist))
+                     relax_obj=L.ptr(self.relax_obj), hist=L.ptr(hist), cycles=L.ptr(self.cycles))
+
+    def enable_phase_timing(self, on=True):
+        """Stamp per-phase shader cycles of every home into self.cycles [NPHASE][N] (diagnostic)."""
+        self.cycles = (torch.zeros((L.NPHASE, self.N), dtype=torch.int64, device=self.device) if on else None)
 
     # ------------------------------------------------------------------ launches
     def step(self, t, noise=None, hist=None, stream=None):

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DRAGG_MPC_ABI_VERSION 1
+#define DRAGG_MPC_ABI_VERSION 2
 
 /* home types (aggregator.py:425, 468, 520, 555); bit 0 = pv, bit 1 = battery */
 enum dragg_home_type {
@@ -143,7 +143,20 @@ typedef struct dragg_mpc_out {
     double* obj;                /* [N] objective sum_k gamma^k price_k p_grid_k         */
     double* relax_obj;          /* [N] LP-relaxation objective (NaN if infeasible)     */
     double* hist;               /* optional [DRAGG_NVAL][N] copy of vals after the step */
+    int64_t* cycles;            /* optional [DRAGG_NPHASE][N] shader cycles per phase   */
 } dragg_mpc_out;
+
+/* solver phases timed into dragg_mpc_out.cycles (diagnostic; NULL = not stamped) */
+enum dragg_phase {
+    DRAGG_PH_SETUP = 0,   /* inputs, problem build, presolve              */
+    DRAGG_PH_ITER,        /* ADMM iterations (rhs, KKT solve, updates)    */
+    DRAGG_PH_FACTOR,      /* block-LDL' factorisations                    */
+    DRAGG_PH_POLISH,      /* exact basis polish                           */
+    DRAGG_PH_CHECK,       /* residuals, certificate, rho adaptation       */
+    DRAGG_PH_INTEGER,     /* integer duty-cycle DP                        */
+    DRAGG_PH_WRITE,       /* objective, cleanup_and_finish, hash writes   */
+    DRAGG_NPHASE
+};
 
 /* explicit per-solve inputs (parity tests and the per-home MPCCalc facade) */
 typedef struct dragg_mpc_explicit {
