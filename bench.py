@@ -35,7 +35,7 @@ def parse():
     ap.add_argument("--homes", type=int, default=1000, help="homes per GPU")
     ap.add_argument("--horizon-hours", type=int, default=6)
     ap.add_argument("--dt", type=int, default=4)
-    ap.add_argument("--int-mode", default="round", choices=["round", "relax"])
+    ap.add_argument("--int-mode", default="round", choices=["round", "relax", "round_lp"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--cpu-workers", type=int, default=0)
     return ap.parse_args()

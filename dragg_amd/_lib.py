@@ -33,9 +33,10 @@ ST_OPTIMAL, ST_INFEASIBLE, ST_INFEASIBLE_CERT, ST_MAX_ITER, ST_ROUND_FAIL, ST_ER
 STATUS_NAMES = ["optimal", "infeasible", "infeasible_cert", "max_iter", "round_fail", "err_parse",
                 "err_missing"]
 
-INT_ROUND, INT_RELAX = 0, 1
+INT_ROUND, INT_RELAX, INT_ROUND_LP = 0, 1, 2
+INT_MODES = {"round": INT_ROUND, "relax": INT_RELAX, "round_lp": INT_ROUND_LP}
 
-PHASES = ["setup", "iter", "factor", "polish", "check", "integer", "write"]
+PHASES = ["setup", "iter", "factor", "polish", "check", "integer", "write", "battery"]
 NPHASE = len(PHASES)
 
 c_dp = ctypes.c_void_p  # device pointers are passed as raw integers

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/dragg_mi355x.h"
 
@@ -104,6 +105,39 @@ DEV double wave_sum(double v) {
     return v;
 }
 DEV bool wave_any(bool p) { return __any(p); }
+
+// order LDS accesses between the lanes of ONE wave (code running on a single wave of a
+// multi-wave workgroup must not use __syncthreads)
+DEV void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// workgroup reductions for nt = 64 * waves threads (red: >= nt / 64 doubles of LDS scratch);
+// the per-wave partials are combined in wave order, so the result is deterministic
+DEV double block_sum(double v, double* red, int lane, int nt) {
+    v = wave_sum(v);
+    if (nt <= WAVE) return v;
+    __syncthreads();
+    if ((lane & (WAVE - 1)) == 0) red[lane / WAVE] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int i = 0; i < nt / WAVE; ++i) s += red[i];
+    __syncthreads();
+    return s;
+}
+DEV double block_max(double v, double* red, int lane, int nt) {
+    v = wave_max(v);
+    if (nt <= WAVE) return v;
+    __syncthreads();
+    if ((lane & (WAVE - 1)) == 0) red[lane / WAVE] = v;
+    __syncthreads();
+    double s = red[0];
+    for (int i = 1; i < nt / WAVE; ++i) s = fmax(s, red[i]);
+    __syncthreads();
+    return s;
+}
 
 // per-phase shader-cycle stamps (dragg_mpc_out.cycles; diagnostic, off when NULL)
 struct Prof {
@@ -955,9 +989,9 @@ DEV double pv_curt(const Lds& L, int k) { return (L.price[k] < 0.0 && L.ghi[k] >
 
 // objective sum_k gamma^k price_k p_grid_k (mpc_calc.py:441-446) for the solution in L.x;
 // also leaves p_grid_k in L.t2[k]
-DEV double objective(const Home& h, const Lds& L, int lane) {
+DEV double objective(const Home& h, const Lds& L, int lane, int nt = WAVE, double* red = nullptr) {
     double s = 0.0;
-    for (int k = lane; k < h.H; k += WAVE) {
+    for (int k = lane; k < h.H; k += nt) {
         const int o = k * 8;
         const double u = L.x[o + S_U], w = L.x[o + S_W];
         const double cc = h.winter ? 0.0 : u, hh = h.winter ? u : 0.0;
@@ -968,7 +1002,7 @@ DEV double objective(const Home& h, const Lds& L, int lane) {
         L.t2[k] = pg;
         s += pow(h.gamma, (double)k) * (L.price[k] * pg);
     }
-    s = wave_sum(s);
+    s = block_sum(s, red, lane, nt);
     __syncthreads();
     return s;
 }
@@ -982,10 +1016,10 @@ struct Io {
 };
 
 // success branch of cleanup_and_finish (mpc_calc.py:486-526)
-DEV void write_success(const Home& h, const Lds& L, const Io& io, int lane) {
+DEV void write_success(const Home& h, const Lds& L, const Io& io, int lane, int nt = WAVE) {
     const int H = h.H;
     const double S = h.S;
-    for (int j = lane; j < H; j += WAVE) {
+    for (int j = lane; j < H; j += nt) {
         const int o = j * 8;
         const double u = L.x[o + S_U], w = L.x[o + S_W];
         const double cc = h.winter ? 0.0 : u, hh = h.winter ? u : 0.0;
@@ -1099,16 +1133,14 @@ struct KArgs {
 };
 
 // --------------------------------------------------------------------------------------
-// the kernel: one workgroup (one wave) per home
+// kernel prologue shared by both solve paths: per-home constants, the step's inputs
+// (get_initial_conditions, water_draws, set_environmental_variables, the season draw).
+// Returns DRAGG_ST_ERR_MISSING where the reference raises KeyError, else -1.
 // --------------------------------------------------------------------------------------
 template <bool EXPLICIT>
-__global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int home = blockIdx.x;
-    const int lane = threadIdx.x;
+DEV int prologue(const KArgs& a, Home& h, const Lds& L, const Io& io, int lane, int nt, double* red) {
+    const int home = io.home;
     const int N = a.d.n_homes;
-    if (home >= N) return;
-    Home h;
     h.H = a.d.horizon; h.S = a.d.sub_steps; h.dt = a.d.dt; h.gamma = a.d.discount;
     h.type = a.p.home_type[home];
     h.pv = (h.type & 1) != 0;
@@ -1116,19 +1148,13 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
     h.nrows = h.batt ? 3 : 2;
     load_params(h, a.p.params, N, home);
     const int H = h.H;
-    Lds L = carve(smem, H);
-    Io io{a.vals, a.fc, N, home};
     int status_pre = -1;
-    Prof pf;
-    pf.start(a.out.cycles != nullptr);
-
-    // ---------------- inputs (get_initial_conditions / set_environmental_variables)
     if (EXPLICIT) {
         h.t = a.ex.t[home];
         h.T0 = a.ex.T0[home]; h.Tw0 = a.ex.Tw0[home]; h.E0 = h.batt ? a.ex.E0[home] : 0.0;
         h.counter = a.ex.counter[home];
         h.winter = a.ex.winter[home] != 0;
-        for (int i = lane; i <= H; i += WAVE) {
+        for (int i = lane; i <= H; i += nt) {
             L.draw[i] = a.ex.draw[(size_t)i * N + home];
             L.oat[i] = a.ex.oat[(size_t)i * N + home];
             L.ghi[i] = a.ex.ghi[(size_t)i * N + home];
@@ -1149,7 +1175,7 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
             const double v = (hh >= 0 && hh < a.d.n_draw_hours) ? a.p.draw_hourly[(size_t)hh * N + home] : 0.0;
             return v / dt;
         };
-        for (int i = lane; i <= H; i += WAVE) {
+        for (int i = lane; i <= H; i += nt) {
             double d;
             if (i < dt) d = rawv(i);
             else if (i + 1 < nraw) d = ((rawv(i - 1) + rawv(i)) + rawv(i + 1)) / 3.0;
@@ -1162,7 +1188,7 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
         }
         // season draw (mpc_calc.py:220-223, 303-309)
         double mx = -INFINITY;
-        for (int k = lane; k < H; k += WAVE) {
+        for (int k = lane; k < H; k += nt) {
             double z;
             if (a.noise) z = a.noise[(size_t)k * N + home];
             else {
@@ -1172,7 +1198,7 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
             }
             mx = fmax(mx, a.p.oat[s0 + k + 1] + pow(1.1, (double)k) * z);
         }
-        mx = wave_max(mx);
+        mx = block_max(mx, red, lane, nt);
         mx = fmax(mx, a.p.oat[s0]);
         h.winter = mx <= 30.0;
         __syncthreads();
@@ -1196,13 +1222,34 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
             if (missing) status_pre = DRAGG_ST_ERR_MISSING;
         }
     }
-    if (status_pre == DRAGG_ST_ERR_MISSING) {
-        if (lane == 0) {
-            a.out.status[home] = DRAGG_ST_ERR_MISSING;
-            a.out.iters[home] = 0;
-            a.out.obj[home] = NAN;
-            a.out.relax_obj[home] = NAN;
-        }
+    return status_pre;
+}
+
+DEV void write_missing(const KArgs& a, int home) {
+    a.out.status[home] = DRAGG_ST_ERR_MISSING;
+    a.out.iters[home] = 0;
+    a.out.obj[home] = NAN;
+    a.out.relax_obj[home] = NAN;
+}
+
+// --------------------------------------------------------------------------------------
+// LP kernel (int_mode relax / round_lp): one workgroup (one wave) per home, ADMM + polish
+// --------------------------------------------------------------------------------------
+template <bool EXPLICIT>
+__global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int home = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int N = a.d.n_homes;
+    if (home >= N) return;
+    Home h;
+    const int H = a.d.horizon;
+    Lds L = carve(smem, H);
+    Io io{a.vals, a.fc, N, home};
+    Prof pf;
+    pf.start(a.out.cycles != nullptr);
+    if (prologue<EXPLICIT>(a, h, L, io, lane, WAVE, nullptr) == DRAGG_ST_ERR_MISSING) {
+        if (lane == 0) write_missing(a, home);
         return;
     }
     derive(h);
@@ -1223,7 +1270,7 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
     if (status == DRAGG_ST_OPTIMAL) {
         relax = objective(h, L, lane);
         pf.mark(DRAGG_PH_WRITE);
-        if (a.d.int_mode == DRAGG_INT_ROUND && !round_duties(h, L, lane)) status = DRAGG_ST_ROUND_FAIL;
+        if (a.d.int_mode == DRAGG_INT_ROUND_LP && !round_duties(h, L, lane)) status = DRAGG_ST_ROUND_FAIL;
         pf.mark(DRAGG_PH_INTEGER);
         if (status == DRAGG_ST_OPTIMAL) obj = objective(h, L, lane);
     }
@@ -1240,6 +1287,669 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
         a.out.iters[home] = iters;
         a.out.obj[home] = obj;
         a.out.relax_obj[home] = relax;
+    }
+    if (a.out.hist && lane == 0)      // lane 0 wrote every vals field of this home
+        for (int k = 0; k < DRAGG_NVAL; ++k) a.out.hist[(size_t)k * N + home] = io.v(k);
+    pf.mark(DRAGG_PH_WRITE);
+    if (pf.on && lane == 0)
+        for (int k = 0; k < DRAGG_NPHASE; ++k) a.out.cycles[(size_t)k * N + home] = (int64_t)pf.acc[k];
+}
+
+// ======================================================================================
+// Direct integer path (int_mode = DRAGG_INT_ROUND, the default).
+//
+// The reference MILP (mpc_calc.py:291-446) is separable: its objective is
+// sum_k gamma^k price_k p_grid_k with p_grid = p_load [+ S(ch + dis)] [- S p_pv], and no
+// constraint couples the thermal variables (T, Tw, hvac/wh duties), the battery
+// (E, ch, dis) and the PV curtailment.  So the MILP optimum is
+//   thermal integer programme (two integer chains)      -> binned forward DP  (dp_thermal)
+// + battery LP (one continuous storage chain)            -> exact convex piecewise-linear
+//                                                           value-function DP (battery_lp)
+// + PV LP (separable per stage)                          -> closed form        (pv_curt)
+// No relaxation / ADMM is needed on this path; the LP kernel above remains the solver of
+// the relaxation (int_mode relax) and of the relaxation-then-round variant (round_lp).
+// ======================================================================================
+constexpr int NB_CAP = 384;          // DP bins per chain (natural count at dt = 4 is <= ~330)
+
+struct LdsD {
+    double *draw, *oat, *ghi, *price;   // [H+1]
+    double *x;                          // [8H] solution in the stage-slot layout of the LP path
+    double *t2;                         // [H] p_grid (objective)
+    double *cA, *cC, *cq;               // [H] coefficients of the chain being solved
+    double *bx0, *bp1, *bp2;            // [H] battery: merged-domain origin, psi segment offsets
+    double *sgS, *sgL;                  // [2][seg_cap] battery segments (slope, length)
+    double2 *lab0, *lab1;               // [NB_CAP] DP labels (cost, exact state), 2 buffers
+    double *sc;                         // [32] scalars / reduction scratch
+    double *rt;                         // [H+1] zero-duty reference trajectory of the chain
+    int *tarr, *inv;                    // [NB_CAP], [NB_CAP+8] DP source keys / inverse table
+    uint16_t* par;                      // [H][NB_CAP] DP back-pointers
+};
+
+__host__ __device__ inline int seg_cap(int H) { return ((2 * H + 2 + 63) / 64) * 64; }
+
+__host__ __device__ inline int direct_lds_bytes(int H) {
+    const int nd = 4 * (H + 1) + 8 * H + H + 3 * H + 3 * H + 4 * seg_cap(H) + 4 * NB_CAP + 32 + (H + 2) + 1;
+    return nd * 8 + (2 * NB_CAP + 8) * 4 + ((H * NB_CAP * 2 + 15) / 16) * 16;
+}
+
+DEV LdsD carve_direct(double* s, int H) {
+    LdsD L;
+    double* const base = s;
+    L.draw = s; s += H + 1;
+    L.oat = s; s += H + 1;
+    L.ghi = s; s += H + 1;
+    L.price = s; s += H + 1;
+    L.x = s; s += 8 * H;
+    L.t2 = s; s += H;
+    L.cA = s; s += H;
+    L.cC = s; s += H;
+    L.cq = s; s += H;
+    L.bx0 = s; s += H;
+    L.bp1 = s; s += H;
+    L.bp2 = s; s += H;
+    const int sc = seg_cap(H);
+    L.sgS = s; s += 2 * sc;
+    L.sgL = s; s += 2 * sc;
+    if ((s - base) & 1) ++s;                                     // 16-B alignment of the labels
+    L.lab0 = reinterpret_cast<double2*>(s); s += 2 * NB_CAP;
+    L.lab1 = reinterpret_cast<double2*>(s); s += 2 * NB_CAP;
+    L.sc = s; s += 32;
+    L.rt = s; s += H + 2;
+    L.tarr = reinterpret_cast<int*>(s);
+    L.inv = L.tarr + NB_CAP;
+    L.par = reinterpret_cast<uint16_t*>(L.inv + NB_CAP + 8);
+    return L;
+}
+
+// the LP path's view (x, t2, environment) for objective / write_success / write_fallback
+DEV Lds lp_view(const LdsD& D) {
+    Lds L{};
+    L.x = D.x; L.t2 = D.t2;
+    L.draw = D.draw; L.oat = D.oat; L.ghi = D.ghi; L.price = D.price;
+    L.sc = D.sc;
+    return L;
+}
+
+// Exact interval feasibility of the T and E chains and the outer test of the Tw chain:
+// presolve_infeasible of the LP path, on the direct path's inputs.
+DEV bool presolve_direct(const Home& h, const LdsD& L, double twlo0, double twhi0) {
+    if (!(h.Twmin <= h.Tw0 && h.Tw0 <= h.Twmax)) return true;          // temp_wh_ev[0] bounds
+    double Tlo = h.T0, Thi = h.T0, Wlo = h.Tw0, Whi = h.Tw0, Elo = h.E0, Ehi = h.E0;
+    const double gS = h.g * h.S;
+    for (int k = 0; k < h.H; ++k) {
+        const double bk = L.oat[k + 1] * h.iR * 3600 * h.inv_c;
+        double lo = h.aT * Tlo + bk + fmin(0.0, gS), hi = h.aT * Thi + bk + fmax(0.0, gS);
+        Tlo = fmax(lo, h.Tmin); Thi = fmin(hi, h.Tmax);
+        if (Tlo > Thi + TOL_P * (1 + fabs(Thi))) return true;
+        const double df = L.draw[k + 1] / h.V, rem = 1 - df, d15 = df * TAP;
+        const double ck = rem + (-rem * h.iRw) * 3600 * h.inv_w;
+        const double dk = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
+        const double wlo = k == 0 ? twlo0 : h.Twmin, whi = k == 0 ? twhi0 : h.Twmax;
+        const double w0 = k == 0 ? h.Tw0 : 0.0;
+        lo = (k == 0 ? ck * w0 : ck * Wlo) + dk + h.e * Tlo;
+        hi = (k == 0 ? ck * w0 : ck * Whi) + dk + h.e * Thi + h.f * h.S;
+        Wlo = fmax(lo, wlo); Whi = fmin(hi, whi);
+        if (Wlo > Whi + TOL_P * (1 + fabs(Whi))) return true;
+        if (h.batt) {
+            lo = Elo - h.brate * (1.0 / h.etad) / h.dt; hi = Ehi + h.brate * h.etac / h.dt;
+            Elo = fmax(lo, h.Emin); Ehi = fmin(hi, h.Emax);
+            if (Elo > Ehi + TOL_P * (1 + fabs(Ehi))) return true;
+        }
+    }
+    return false;
+}
+
+// --------------------------------------------------------------------------------------
+// Thermal integer chain  x_{k+1} = A_k x_k + g u_k + C_k,  u_k in {0..S},  x_{k+1} in box_k,
+// minimise sum_k cq_k u_k.  Forward DP over the state discretised into nb bins of width w
+// (1/NBU of one duty unit's effect, or wider if the box needs more than NB_CAP bins); each
+// bin keeps its cheapest label with its EXACT state, so every kept path is exactly
+// feasible and costed (a bin collision is the only approximation).  Pull form: the thread
+// owning target bin B scans, per duty u, the source bins whose states can land in B (the
+// map is monotone, A_k > 0: ceil(1/A_k) + 2 candidates, 3 while A_k > 1/2), so a stage is
+// conflict-free; labels are double-buffered, one barrier per stage.  Back-pointer byte =
+// u | (source - first candidate) << 4, decoded by recomputing the first candidate.
+// --------------------------------------------------------------------------------------
+struct DpGeom {
+    double glo, w, iw;
+    int nb;
+};
+
+DEV DpGeom dp_geom(double glo, double ghi, double g) {
+    DpGeom G;
+    G.glo = glo;
+    G.w = fabs(g) / NBU;
+    G.nb = (int)floor((ghi - glo) / G.w) + 1;
+    if (G.nb > NB_CAP) { G.w = (ghi - glo) / (NB_CAP - 1); G.nb = NB_CAP; }
+    G.iw = 1.0 / G.w;
+    return G;
+}
+
+// first candidate source bin for target bin B at a stage with A (iA = 1/A) and
+// base = g u + C: states below (bin_lo(B) - base) / A cannot reach B
+DEV int dp_first_source(const DpGeom& G, int B, double iA, double base) {
+    const double xa = (G.glo + B * G.w - base) * iA;
+    return (int)floor((xa - G.glo) * G.iw - 1e-7);
+}
+
+template <int SS>
+DEV bool dp_fixed(const Home& h, LdsD& L, int lane, int nt, double g, double x0, double lo0, double hi0,
+                    double lo, double hi, int sx, int sv) {
+    constexpr int NU = SS > 0 ? SS + 1 : 16;
+    const int H = h.H;
+    const int S = SS > 0 ? SS : h.S;
+    const DpGeom G = dp_geom(fmin(lo0, lo), fmax(hi0, hi), g);
+    const int nb = G.nb;
+    double2* cur = L.lab0;
+    double2* nxt = L.lab1;
+    const double BIG = INFINITY;
+    for (int k = 0; k < H; ++k) {
+        const double Ak = L.cA[k], Ck = L.cC[k], ck = L.cq[k];
+        const double blo = k == 0 ? lo0 : lo, bhi = k == 0 ? hi0 : hi;
+        const double tlo = blo - TOL_P * (1 + fabs(blo)), thi = bhi + TOL_P * (1 + fabs(bhi));
+        const double iA = 1.0 / Ak;
+        // the offset is stored in 4 bits: A_k < 1/14 (a tank nearly emptied in one step)
+        // caps the window at 16 candidates
+        const int ncand = (int)fmin(16.0, ceil(iA) + 2.0);
+        for (int B = lane; B < nb; B += nt) {
+            const double fB = (double)B, fB1 = (double)(B + 1);
+            double best = BIG, bx = 0.0;
+            int bp = 0xFF;
+            // label x lands in bin B  <=>  floor((x - glo) / w) == B  <=>  B <= t < B + 1
+            auto consider = [&](double xn, double cn, int code) {
+                const double t = (xn - G.glo) * G.iw;
+                const bool ok = (xn >= tlo) & (xn <= thi) & (t >= fB) & (t < fB1) & (cn < best);
+                best = ok ? cn : best;
+                bx = ok ? xn : bx;
+                bp = ok ? code : bp;
+            };
+            if (k == 0) {
+                for (int u = 0; u <= S; ++u)
+                    consider(fma(Ak, x0, fma(g, (double)u, Ck)), ck * u, u);
+            } else if (SS > 0 && ncand == 3) {
+                // all loads first (one 16-B label per candidate), then branch-free selects
+                double2 lv[NU][3];
+                double base[NU];
+                int s0[NU];
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    base[u] = fma(g, (double)u, Ck);
+                    s0[u] = dp_first_source(G, B, iA, base[u]);
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) {
+                        const int sb = min(max(s0[u] + d, 0), nb - 1);
+                        lv[u][d] = cur[sb];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < NU; ++u)
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) {
+                        const int sb = s0[u] + d;
+                        const double cs = (sb >= 0 && sb < nb) ? lv[u][d].x : BIG;
+                        consider(fma(Ak, lv[u][d].y, base[u]), fma(ck, (double)u, cs), u | (d << 4));
+                    }
+            } else {
+                for (int u = 0; u <= S; ++u) {
+                    const double bs = fma(g, (double)u, Ck);
+                    const int s0 = dp_first_source(G, B, iA, bs);
+                    for (int d = 0; d < ncand; ++d) {
+                        const int sb = s0 + d;
+                        const double2 lv = cur[min(max(sb, 0), nb - 1)];
+                        const double cs = (sb >= 0 && sb < nb) ? lv.x : BIG;
+                        consider(fma(Ak, lv.y, bs), fma(ck, (double)u, cs), u | (d << 4));
+                    }
+                }
+            }
+            nxt[B] = make_double2(best, bx);
+            L.par[k * NB_CAP + B] = (uint16_t)bp;
+        }
+        __syncthreads();
+        double2* t = cur; cur = nxt; nxt = t;
+    }
+    // cheapest final label (lowest bin on ties, deterministic)
+    double best = BIG;
+    int bb = -1;
+    for (int B = lane; B < nb; B += nt)
+        if (cur[B].x < best) { best = cur[B].x; bb = B; }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bb, o);
+        if (ob < best || (ob == best && oi >= 0 && (bb < 0 || oi < bb))) { best = ob; bb = oi; }
+    }
+    if (nt > WAVE) {
+        int* ri = reinterpret_cast<int*>(L.sc + 16);
+        if ((lane & (WAVE - 1)) == 0) { L.sc[lane / WAVE] = best; ri[lane / WAVE] = bb; }
+        __syncthreads();
+        best = L.sc[0]; bb = ri[0];
+        for (int i = 1; i < nt / WAVE; ++i) {
+            const double ob = L.sc[i];
+            const int oi = ri[i];
+            if (ob < best || (ob == best && oi >= 0 && (bb < 0 || oi < bb))) { best = ob; bb = oi; }
+        }
+        __syncthreads();
+    }
+    if (bb < 0) return false;
+    if (lane == 0) {
+        int b = bb;
+        for (int k = H - 1; k >= 0; --k) {
+            const int p = L.par[k * NB_CAP + b];
+            const int u = p & 15;
+            L.x[k * 8 + sv] = (double)u;
+            if (k > 0) b = dp_first_source(G, b, 1.0 / L.cA[k], fma(g, (double)u, L.cC[k])) + (p >> 4);
+        }
+        double x = x0;                      // exact forward trajectory of the chosen duties
+        for (int k = 0; k < H; ++k) {
+            x = fma(L.cA[k], x, fma(g, L.x[k * 8 + sv], L.cC[k]));
+            L.x[k * 8 + sx] = x;
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
+// --------------------------------------------------------------------------------------
+// The same DP on buckets that move with the chain's zero-duty reference trajectory
+// r_{k+1} = A_k r_k + C_k.  With z = (x - r_k)/w + c_k (c_0 = 1/2, c_{k+1} = A_k c_k) the
+// dynamics become z' = A_k z + sh*u with sh = +-NBU an integer (w = |g|/NBU), so a label's
+// target bucket is floor(A_k z) + sh*u: ONE key T_s = floor(A_k z_s) per source bucket, and
+// the sources of (target b, duty u) are exactly the run {s : T_s = b - sh*u} (1-2 buckets,
+// found through an inverse table).  Labels keep their EXACT state x, as in dp_fixed, and
+// every kept path is exactly feasible; buckets are the only approximation.  Each stage:
+// keys -> inverse table -> pull over target buckets; three barriers.
+// Returns 1 solved, 0 no integer schedule, -1 geometry unsupported (more than NB_CAP
+// buckets: the caller uses dp_fixed with wider bins).
+// --------------------------------------------------------------------------------------
+template <int SS>
+DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0, double lo0, double hi0,
+                  double lo, double hi, int sx, int sv) {
+    constexpr int NU = SS > 0 ? SS + 1 : 16;
+    const int H = h.H;
+    const int S = SS > 0 ? SS : h.S;
+    const double w = fabs(g) / NBU, iw = 1.0 / w;
+    const int sh = g > 0.0 ? NBU : -NBU;
+    const double BIG = INFINITY;
+    {
+        const double tl = lo - TOL_P * (1 + fabs(lo)), th = hi + TOL_P * (1 + fabs(hi));
+        if ((th - tl) * iw + 4.0 > (double)NB_CAP) return -1;
+    }
+    if (lane == 0) {
+        double r = x0;
+        L.rt[0] = r;
+        for (int k = 0; k < H; ++k) {
+            r = fma(L.cA[k], r, L.cC[k]);
+            L.rt[k + 1] = r;
+        }
+    }
+    __syncthreads();
+    // bucket window of the labels x_{k+1} (tolerance-widened box, one bucket of margin)
+    auto window = [&](int k, double c1, int* blo) -> int {
+        const double bl = k == 0 ? lo0 : lo, bh = k == 0 ? hi0 : hi;
+        const double tl = bl - TOL_P * (1 + fabs(bl)), th = bh + TOL_P * (1 + fabs(bh));
+        const double r = L.rt[k + 1];
+        *blo = (int)floor((tl - r) * iw + c1) - 1;
+        return (int)floor((th - r) * iw + c1) + 1 - *blo + 1;
+    };
+    double2* cur = L.lab0;
+    double2* nxt = L.lab1;
+    // stage 0: from the single initial label (z = 1/2) to buckets sh*u + floor(A_0 / 2) = sh*u
+    double c = 0.5;
+    double cn1 = L.cA[0] * c;
+    int blo;
+    int nbz = window(0, cn1, &blo);
+    {
+        const double A0 = L.cA[0], C0 = L.cC[0], q0 = L.cq[0];
+        const double tl = lo0 - TOL_P * (1 + fabs(lo0)), th = hi0 + TOL_P * (1 + fabs(hi0));
+        for (int j = lane; j < nbz; j += nt) { cur[j] = make_double2(BIG, 0.0); L.par[j] = 0xFFFF; }
+        __syncthreads();
+        for (int u = lane; u <= S; u += nt) {
+            const int j = sh * u + (int)floor(cn1) - blo;
+            const double xn = fma(A0, x0, fma(g, (double)u, C0));
+            if (j >= 0 && j < nbz && xn >= tl && xn <= th) {
+                cur[j] = make_double2(q0 * u, xn);
+                L.par[j] = (uint16_t)(u << 12);
+            }
+        }
+        __syncthreads();
+    }
+    c = cn1;
+    for (int k = 1; k < H; ++k) {
+        const double Ak = L.cA[k], Ck = L.cC[k], ck = L.cq[k];
+        const double tl = lo - TOL_P * (1 + fabs(lo)), th = hi + TOL_P * (1 + fabs(hi));
+        const double rk = L.rt[k];
+        // (a) source keys T_s = floor(A_k z_s), z clamped into the bucket (keeps T monotone);
+        //     an empty bucket uses its centre
+        for (int s = lane; s < nbz; s += nt) {
+            const double2 lv = cur[s];
+            const double b = (double)(blo + s);
+            double zz = lv.x < BIG ? (lv.y - rk) * iw + c : b + 0.5;
+            zz = fmin(fmax(zz, b), b + 0.999999);
+            L.tarr[s] = (int)floor(Ak * zz);
+        }
+        __syncthreads();
+        // (b) inverse table: inv[m - mlo] = first source with T >= m, inv[mhi - mlo + 1] = nbz
+        const int mlo = L.tarr[0], mhi = L.tarr[nbz - 1];
+        for (int s = lane; s < nbz; s += nt) {
+            const int T = L.tarr[s];
+            const int Tp = s > 0 ? L.tarr[s - 1] : mlo - 1;
+            for (int m = Tp + 1; m <= T; ++m) L.inv[m - mlo] = s;
+            if (s == nbz - 1) L.inv[mhi - mlo + 1] = nbz;
+        }
+        __syncthreads();
+        // (c) targets
+        const double c1 = Ak * c;
+        int blo1;
+        const int nbz1 = window(k, c1, &blo1);
+        for (int j = lane; j < nbz1; j += nt) {
+            const int b = blo1 + j;
+            double best = BIG, bx = 0.0;
+            int bp = 0xFFFF;
+            auto consider = [&](double2 lv, double base, int u, int src) {
+                const double xn = fma(Ak, lv.y, base);
+                const double cn = fma(ck, (double)u, lv.x);
+                const bool ok = (xn >= tl) & (xn <= th) & (cn < best);
+                best = ok ? cn : best;
+                bx = ok ? xn : bx;
+                bp = ok ? (src | (u << 12)) : bp;
+            };
+            if constexpr (SS > 0) {
+                int sa[NU], sb[NU];
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const int m = b - sh * u;
+                    const bool in = m >= mlo && m <= mhi;
+                    const int mi = in ? m - mlo : 0;
+                    sa[u] = in ? L.inv[mi] : 0;
+                    sb[u] = in ? L.inv[mi + 1] : 0;
+                }
+                double2 l0[NU], l1[NU];
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    l0[u] = cur[min(sa[u], nbz - 1)];
+                    l1[u] = cur[min(sa[u] + 1, nbz - 1)];
+                }
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const double base = fma(g, (double)u, Ck);
+                    if (sa[u] < sb[u]) consider(l0[u], base, u, sa[u]);
+                    if (sa[u] + 1 < sb[u]) consider(l1[u], base, u, sa[u] + 1);
+                    for (int s2 = sa[u] + 2; s2 < sb[u]; ++s2) consider(cur[s2], base, u, s2);
+                }
+            } else {
+                for (int u = 0; u <= S; ++u) {
+                    const int m = b - sh * u;
+                    if (m < mlo || m > mhi) continue;
+                    const double base = fma(g, (double)u, Ck);
+                    for (int s2 = L.inv[m - mlo]; s2 < L.inv[m - mlo + 1]; ++s2) consider(cur[s2], base, u, s2);
+                }
+            }
+            nxt[j] = make_double2(best, bx);
+            L.par[k * NB_CAP + j] = (uint16_t)bp;
+        }
+        __syncthreads();
+        double2* t = cur; cur = nxt; nxt = t;
+        blo = blo1; nbz = nbz1; c = c1;
+    }
+    // cheapest final label (lowest bucket on ties, deterministic)
+    double best = BIG;
+    int bb = -1;
+    for (int j = lane; j < nbz; j += nt)
+        if (cur[j].x < best) { best = cur[j].x; bb = j; }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bb, o);
+        if (ob < best || (ob == best && oi >= 0 && (bb < 0 || oi < bb))) { best = ob; bb = oi; }
+    }
+    if (nt > WAVE) {
+        int* ri = reinterpret_cast<int*>(L.sc + 16);
+        if ((lane & (WAVE - 1)) == 0) { L.sc[lane / WAVE] = best; ri[lane / WAVE] = bb; }
+        __syncthreads();
+        best = L.sc[0]; bb = ri[0];
+        for (int i = 1; i < nt / WAVE; ++i) {
+            const double ob = L.sc[i];
+            const int oi = ri[i];
+            if (ob < best || (ob == best && oi >= 0 && (bb < 0 || oi < bb))) { best = ob; bb = oi; }
+        }
+        __syncthreads();
+    }
+    if (bb < 0) return 0;
+    if (lane == 0) {
+        int j = bb;
+        for (int k = H - 1; k >= 0; --k) {
+            const int p = L.par[k * NB_CAP + j];
+            L.x[k * 8 + sv] = (double)(p >> 12);
+            j = p & 0xFFF;
+        }
+        double x = x0;                      // exact forward trajectory (the labels' arithmetic)
+        for (int k = 0; k < H; ++k) {
+            x = fma(L.cA[k], x, fma(g, L.x[k * 8 + sv], L.cC[k]));
+            L.x[k * 8 + sx] = x;
+        }
+    }
+    __syncthreads();
+    return 1;
+}
+
+template <int SS>
+DEV bool dp_thermal(const Home& h, LdsD& L, int lane, int nt, double g, double x0, double lo0, double hi0,
+                    double lo, double hi, int sx, int sv) {
+    const int r = dp_zspace<SS>(h, L, lane, nt, g, x0, lo0, hi0, lo, hi, sx, sv);
+    if (r >= 0) return r == 1;
+    return dp_fixed<SS>(h, L, lane, nt, g, x0, lo0, hi0, lo, hi, sx, sv);
+}
+
+// --------------------------------------------------------------------------------------
+// Battery LP (mpc_calc.py:355-373 with its p_grid / cost terms): min sum_k q_k (ch_k + dis_k),
+// E_{k+1} = E_k + a ch_k + b dis_k (a = eta_c/dt, b = 1/(eta_d dt)), 0 <= ch <= r,
+// -r <= dis <= 0, Emin <= E_{1..H} <= Emax, q_k = S gamma^k price_k.
+// The cost-to-go V_k(E) is convex piecewise linear.  With psi_k(z) the cheapest cost of
+// moving E_k -> E_k - z in one stage (two linear pieces: charge / discharge, or for q < 0
+// the charge-while-discharging edge), V_k = clip(V_{k+1} [inf-convolution] psi_k): the
+// sorted (slope, length) segment list of V_{k+1} merged with psi_k's two segments, then
+// cut to [Emin, Emax].  Each stage is a rank count + a scatter + a prefix scan on one wave.
+// Recovery needs, per stage, only the merged domain origin and the offsets of psi_k's two
+// segments in the merged order: the optimal split of a position p along the merged list
+// takes psi's share of the first p units of length.  Exact, no iteration.
+// Runs on one wave; at most 2H + 1 segments.
+// --------------------------------------------------------------------------------------
+DEV void battery_psi(const Home& h, double q, double* s1, double* l1, double* s2, double* l2) {
+    const double a = h.etac / h.dt, b = (1.0 / h.etad) / h.dt, r = h.brate;
+    if (q >= 0.0) { *s1 = -q / a; *l1 = a * r; *s2 = -q / b; *l2 = b * r; }   // charge | discharge
+    else          { *s1 = -q / b; *l1 = b * r; *s2 = -q / a; *l2 = a * r; }   // full-charge edge first
+}
+
+DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
+    const int H = h.H;
+    const int cap = seg_cap(H);
+    const double a = h.etac / h.dt, b = (1.0 / h.etad) / h.dt, r = h.brate;
+    const double x0psi = -a * r;
+    double* S0 = L.sgS;  double* L0 = L.sgL;          // current list
+    double* S1 = L.sgS + cap; double* L1 = L.sgL + cap;
+    int n = 1;
+    double x0 = h.Emin;                               // V_H: free terminal state, slope 0
+    if (lane == 0) { S0[0] = 0.0; L0[0] = h.Emax - h.Emin; }
+    wave_sync();
+    bool feasible = true;
+    for (int k = H - 1; k >= 0; --k) {
+        double s1, l1, s2, l2;
+        battery_psi(h, L.cq[k], &s1, &l1, &s2, &l2);
+        // ranks: psi's segments go after existing segments of equal slope
+        int c1 = 0, c2 = 0;
+        double p1 = 0.0, p2 = 0.0;
+        for (int i = lane; i < n; i += WAVE) {
+            const double si = S0[i], li = L0[i];
+            if (si <= s1) { ++c1; p1 += li; }
+            if (si <= s2) { ++c2; p2 += li; }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            c1 += __shfl_xor(c1, o); c2 += __shfl_xor(c2, o);
+            p1 += __shfl_xor(p1, o); p2 += __shfl_xor(p2, o);
+        }
+        const int r1 = c1, r2 = c2 + 1;               // merged positions of psi's segments
+        p2 += l1;                                     // psi 1 precedes psi 2 (s1 <= s2)
+        for (int i = lane; i < n; i += WAVE) {
+            const double si = S0[i];
+            const int j = i + (s1 < si ? 1 : 0) + (s2 < si ? 1 : 0);
+            S1[j] = si; L1[j] = L0[i];
+        }
+        if (lane == 0) { S1[r1] = s1; L1[r1] = l1; S1[r2] = s2; L1[r2] = l2; }
+        const double X0M = x0 + x0psi;
+        if (lane == 0) { L.bx0[k] = X0M; L.bp1[k] = p1; L.bp2[k] = p2; }
+        n += 2;
+        wave_sync();
+        double tot = 0.0;
+        for (int i = lane; i < n; i += WAVE) tot += L1[i];
+        tot = wave_sum(tot);
+        if (k == 0) {                                 // E_0 is fixed: it must lie in the domain
+            const double p = h.E0 - X0M;
+            feasible = p >= -TOL_P * (1 + fabs(h.E0)) && p <= tot + TOL_P * (1 + fabs(h.E0));
+            break;
+        }
+        // cut the merged list to E_k in [Emin, Emax] (k >= 1)
+        const double cl = fmax(0.0, h.Emin - X0M), chi = fmin(tot, h.Emax - X0M);
+        if (!(cl <= chi + TOL_P * (1 + fabs(h.Emax)))) { feasible = false; break; }
+        // exclusive prefix of lengths in list order (lane-contiguous chunks)
+        const int per = (n + WAVE - 1) / WAVE;
+        const int i0 = lane * per, i1 = min(n, i0 + per);
+        double loc = 0.0;
+        for (int i = i0; i < i1; ++i) loc += L1[i];
+        double inc = loc;
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const double v = __shfl_up(inc, o);
+            if (lane >= o) inc += v;
+        }
+        double pre = inc - loc;
+        int first = n, last = -1;
+        for (int i = i0; i < i1; ++i) {
+            const double st = pre, en = pre + L1[i];
+            const double ns = fmax(st, cl), ne = fmin(en, chi);
+            if (ne > ns) { first = min(first, i); last = max(last, i); }
+            L1[i] = fmax(0.0, ne - ns);
+            pre = en;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            first = min(first, __shfl_xor(first, o));
+            last = max(last, __shfl_xor(last, o));
+        }
+        wave_sync();
+        const int nn = last >= first ? last - first + 1 : 0;
+        for (int i = lane; i < nn; i += WAVE) { S0[i] = S1[first + i]; L0[i] = L1[first + i]; }
+        if (nn == 0 && lane == 0) { S0[0] = 0.0; L0[0] = 0.0; }   // a single feasible point
+        n = nn == 0 ? 1 : nn;
+        x0 = X0M + cl;
+        wave_sync();
+    }
+    if (!feasible) return false;
+    if (lane == 0) {                                  // forward recovery of E, ch, dis
+        double E = h.E0;
+        for (int k = 0; k < H; ++k) {
+            double s1, l1, s2, l2;
+            battery_psi(h, L.cq[k], &s1, &l1, &s2, &l2);
+            const double p = E - L.bx0[k];
+            const double z = x0psi + fmin(fmax(p - L.bp1[k], 0.0), l1) + fmin(fmax(p - L.bp2[k], 0.0), l2);
+            const double dlt = -z;                   // E_{k+1} - E_k
+            double chv, dis;
+            if (L.cq[k] >= 0.0) {
+                if (dlt >= 0.0) { chv = fmin(dlt / a, r); dis = 0.0; }
+                else            { chv = 0.0; dis = fmax(dlt / b, -r); }
+            } else {
+                chv = fmin(r, (dlt + b * r) / a);
+                dis = fmax(-r, fmin(0.0, (dlt - a * chv) / b));
+            }
+            E = E + (h.etac * chv + dis / h.etad) / h.dt;   // mpc_calc.py:363-365
+            L.x[k * 8 + S_CH] = chv;
+            L.x[k * 8 + S_DIS] = dis;
+            L.x[k * 8 + S_E] = E;
+        }
+    }
+    wave_sync();
+    return true;
+}
+
+template <bool EXPLICIT, int NT>
+__global__ __launch_bounds__(NT) void mpc_direct_kernel(KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int home = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int N = a.d.n_homes;
+    if (home >= N) return;
+    Home h;
+    const int H = a.d.horizon;
+    LdsD D = carve_direct(smem, H);
+    Lds L = lp_view(D);
+    Io io{a.vals, a.fc, N, home};
+    Prof pf;
+    pf.start(a.out.cycles != nullptr);
+    if (prologue<EXPLICIT>(a, h, L, io, lane, NT, D.sc) == DRAGG_ST_ERR_MISSING) {
+        if (lane == 0) write_missing(a, home);
+        return;
+    }
+    derive(h);
+    // temp_wh (the un-mixed one-step value, mpc_calc.py:336-340) differs from Tw_1 by a
+    // constant Kc, so its bounds become a tightened box on Tw_1 (as in build()).
+    double twlo0, twhi0;
+    {
+        const double rem1 = 1 - D.draw[1] / h.V;
+        const double c0 = rem1 + (-rem1 * h.iRw) * 3600 * h.inv_w;
+        const double d15 = D.draw[1] / h.V * TAP;
+        const double d0 = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
+        const double Kc = (h.Tw0 + ((-h.Tw0) * h.iRw) * 3600 * h.inv_w) - c0 * h.Tw0 - d0;
+        twlo0 = fmax(h.Twmin, h.Twmin - Kc);
+        twhi0 = fmin(h.Twmax, h.Twmax - Kc);
+    }
+    int status = presolve_direct(h, D, twlo0, twhi0) ? DRAGG_ST_INFEASIBLE : DRAGG_ST_OPTIMAL;
+    pf.mark(DRAGG_PH_SETUP);
+    double obj = NAN;
+    if (status == DRAGG_ST_OPTIMAL) {
+        // indoor air chain (mpc_calc.py:314-317); u = duty of the season's mode (:303-309)
+        for (int k = lane; k < H; k += NT) {
+            D.cA[k] = h.aT;
+            D.cC[k] = D.oat[k + 1] * h.iR * 3600 * h.inv_c;
+            D.cq[k] = pow(h.gamma, (double)k) * D.price[k] * h.Pact;
+            D.x[k * 8 + S_PAD] = 0.0;
+            D.x[k * 8 + S_CH] = 0.0; D.x[k * 8 + S_DIS] = 0.0; D.x[k * 8 + S_E] = 0.0;
+        }
+        __syncthreads();
+        bool ok;
+        if (h.S == 6) ok = dp_thermal<6>(h, D, lane, NT, h.g, h.T0, h.Tmin, h.Tmax, h.Tmin, h.Tmax, S_T, S_U);
+        else ok = dp_thermal<0>(h, D, lane, NT, h.g, h.T0, h.Tmin, h.Tmax, h.Tmin, h.Tmax, S_T, S_U);
+        // water-heater chain given T (mpc_calc.py:330-332)
+        if (ok) {
+            for (int k = lane; k < H; k += NT) {
+                const double df = D.draw[k + 1] / h.V, rem = 1 - df, d15 = df * TAP;
+                D.cA[k] = rem + (-rem * h.iRw) * 3600 * h.inv_w;
+                D.cC[k] = h.e * D.x[k * 8 + S_T] + (d15 + ((-d15) * h.iRw) * 3600 * h.inv_w);
+                D.cq[k] = pow(h.gamma, (double)k) * D.price[k] * (h.S * h.Pw);
+            }
+            __syncthreads();
+            if (h.S == 6) ok = dp_thermal<6>(h, D, lane, NT, h.f, h.Tw0, twlo0, twhi0, h.Twmin, h.Twmax, S_TW, S_W);
+            else ok = dp_thermal<0>(h, D, lane, NT, h.f, h.Tw0, twlo0, twhi0, h.Twmin, h.Twmax, S_TW, S_W);
+        }
+        pf.mark(DRAGG_PH_INTEGER);
+        if (!ok) status = DRAGG_ST_ROUND_FAIL;
+        if (ok && h.batt) {
+            for (int k = lane; k < H; k += NT) D.cq[k] = pow(h.gamma, (double)k) * D.price[k] * h.S;
+            __syncthreads();
+            bool bok = true;
+            if (lane < WAVE) bok = battery_lp(h, D, lane);
+            if (lane == 0) D.sc[31] = bok ? 1.0 : 0.0;
+            __syncthreads();
+            if (D.sc[31] == 0.0) status = DRAGG_ST_INFEASIBLE;
+            __syncthreads();
+        }
+        pf.mark(DRAGG_PH_BATTERY);
+        if (status == DRAGG_ST_OPTIMAL) obj = objective(h, L, lane, NT, D.sc);
+    }
+    if (status == DRAGG_ST_OPTIMAL) {
+        write_success(h, L, io, lane, NT);
+    } else if (lane == 0) {
+        status = write_fallback(h, L, io, status);
+    }
+    if (lane == 0) {
+        a.out.status[home] = status;
+        a.out.iters[home] = 0;
+        a.out.obj[home] = obj;
+        a.out.relax_obj[home] = NAN;
     }
     if (a.out.hist && lane == 0)      // lane 0 wrote every vals field of this home
         for (int k = 0; k < DRAGG_NVAL; ++k) a.out.hist[(size_t)k * N + home] = io.v(k);
@@ -1278,26 +1988,53 @@ __global__ void noise_kernel(int N, int H, uint64_t seed, int off, int t, double
     if (2 * pr + 1 < H) out[(size_t)(2 * pr + 1) * N + home] = z1;
 }
 
+bool direct_mode(const dragg_mpc_dims* d) { return d->int_mode == DRAGG_INT_ROUND; }
+
+size_t kernel_lds_bytes(const dragg_mpc_dims* d) {
+    return direct_mode(d) ? (size_t)direct_lds_bytes(d->horizon) : (size_t)lds_doubles(d->horizon) * 8;
+}
+
 int check_dims(const dragg_mpc_dims* d) {
     if (!d || d->n_homes < 0 || d->horizon < 1 || d->sub_steps < 1 || d->dt < 1) return DRAGG_E_ARG;
-    if ((size_t)lds_doubles(d->horizon) * 8 > 160 * 1024) return DRAGG_E_HORIZON;
+    if (d->int_mode < DRAGG_INT_ROUND || d->int_mode > DRAGG_INT_ROUND_LP) return DRAGG_E_ARG;
+    if (direct_mode(d) && d->sub_steps > 15) return DRAGG_E_ARG;     // 4-bit duty in the DP record
+    if (kernel_lds_bytes(d) > 160 * 1024) return DRAGG_E_HORIZON;
     return DRAGG_OK;
+}
+
+// threads per home of the direct kernel (64, 128 or 256); DRAGG_DIRECT_THREADS overrides
+int direct_threads() {
+    static int nt = 0;
+    if (nt == 0) {
+        const char* e = getenv("DRAGG_DIRECT_THREADS");
+        const int v = e ? atoi(e) : 0;
+        nt = (v == 128 || v == 256) ? v : 64;
+    }
+    return nt;
+}
+
+template <typename K>
+int launch_kernel(K kern, int& attr_state, const KArgs& a, int nt, hipStream_t s) {
+    if (!attr_state) {
+        if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+            hipSuccess)
+            return DRAGG_E_LDS;
+        attr_state = 1;
+    }
+    if (a.d.n_homes == 0) return DRAGG_OK;
+    hipLaunchKernelGGL(kern, dim3(a.d.n_homes), dim3(nt), kernel_lds_bytes(&a.d), s, a);
+    return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
 }
 
 template <bool EXPLICIT>
 int launch(const KArgs& a, hipStream_t s) {
-    const int H = a.d.horizon;
-    const size_t lds = (size_t)lds_doubles(H) * 8;
-    static bool attr_set[2] = {false, false};
-    if (!attr_set[EXPLICIT ? 1 : 0]) {
-        if (hipFuncSetAttribute((const void*)mpc_home_kernel<EXPLICIT>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-            return DRAGG_E_LDS;
-        attr_set[EXPLICIT ? 1 : 0] = true;
+    static int attr[4] = {0, 0, 0, 0};
+    if (!direct_mode(&a.d)) return launch_kernel(mpc_home_kernel<EXPLICIT>, attr[0], a, 64, s);
+    switch (direct_threads()) {
+        case 128: return launch_kernel(mpc_direct_kernel<EXPLICIT, 128>, attr[2], a, 128, s);
+        case 256: return launch_kernel(mpc_direct_kernel<EXPLICIT, 256>, attr[3], a, 256, s);
+        default: return launch_kernel(mpc_direct_kernel<EXPLICIT, 64>, attr[1], a, 64, s);
     }
-    if (a.d.n_homes == 0) return DRAGG_OK;
-    hipLaunchKernelGGL(mpc_home_kernel<EXPLICIT>, dim3(a.d.n_homes), dim3(64), lds, s, a);
-    return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
 }
 
 }  // namespace
@@ -1320,7 +2057,7 @@ const char* dragg_mpc_strerror(int code) {
 int dragg_mpc_lds_bytes(const dragg_mpc_dims* dims) {
     const int rc = check_dims(dims);
     if (rc) return rc;
-    return lds_doubles(dims->horizon) * 8;
+    return (int)kernel_lds_bytes(dims);
 }
 
 int dragg_mpc_step(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob, dragg_mpc_hash* hash,

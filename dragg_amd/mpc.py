@@ -91,12 +91,16 @@ class MPCBatch:
     oat, ghi, tou : full-length redis lists (aggregator.py:653-662), any sequence of floats.
     start_index : `start_hour_index` (aggregator.py:630-638).
     reward_price : the redis 'reward_price' list (length 1 or >= H, mpc_calc.py:353).
-    int_mode : 'round' (relaxation + feasible rounding of the integer duty cycles) or 'relax'.
+    int_mode : 'round' (default: the reference MILP -- thermal integer duty cycles by DP, the
+        battery LP by an exact piecewise-linear DP), 'relax' (the LP relaxation by ADMM + exact
+        vertex polish) or 'round_lp' (the relaxation for status / battery, then the integer DP).
     seed : key of the on-device season-noise stream used when no noise is supplied.
     """
 
     def __init__(self, homes, oat=None, ghi=None, tou=None, start_index=0, reward_price=(0.0,),
                  int_mode="round", seed=0, max_iter=4000, check_every=10, device="cuda", home_offset=0):
+        if int_mode not in L.INT_MODES:
+            raise ValueError(f"int_mode must be one of {sorted(L.INT_MODES)}, not {int_mode!r}")
         self.lib = L.load()
         if not torch.cuda.is_available():
             raise L.DraggError("no GPU visible: the batched MPC has no CPU fallback")
@@ -112,7 +116,7 @@ class MPCBatch:
         self.draws = torch.tensor(draws, dtype=torch.float64, device=dev).contiguous()
         self.dims = L.Dims(n_homes=self.N, horizon=self.H, sub_steps=self.S, dt=self.dt,
                            n_draw_hours=dm["n_draw_hours"], n_env=0, n_rp=1,
-                           int_mode=L.INT_ROUND if int_mode == "round" else L.INT_RELAX,
+                           int_mode=L.INT_MODES[int_mode],
                            max_iter=max_iter, check_every=check_every, discount=dm["discount"])
         self.seed = int(seed)
         self.home_offset = int(home_offset)

@@ -101,8 +101,9 @@ enum dragg_mpc_error {
 
 /* integer handling of the duty-cycle variables (mpc_calc.py:171-173) */
 enum dragg_int_mode {
-    DRAGG_INT_ROUND = 0,   /* relaxation + feasibility-preserving rounding (default)  */
-    DRAGG_INT_RELAX = 1    /* report the LP relaxation                                */
+    DRAGG_INT_ROUND = 0,    /* MILP: thermal integer DP + exact battery LP (default)   */
+    DRAGG_INT_RELAX = 1,    /* LP relaxation (ADMM + exact vertex polish)             */
+    DRAGG_INT_ROUND_LP = 2  /* LP relaxation for status/battery, then the integer DP  */
 };
 
 typedef struct dragg_mpc_dims {
@@ -155,6 +156,7 @@ enum dragg_phase {
     DRAGG_PH_CHECK,       /* residuals, certificate, rho adaptation       */
     DRAGG_PH_INTEGER,     /* integer duty-cycle DP                        */
     DRAGG_PH_WRITE,       /* objective, cleanup_and_finish, hash writes   */
+    DRAGG_PH_BATTERY,     /* exact battery LP (int_mode round)            */
     DRAGG_NPHASE
 };
 

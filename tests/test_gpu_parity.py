@@ -37,11 +37,25 @@ def _solve(d, records, int_mode):
                 iters=b.iters.cpu().numpy(), vals=b.vals.cpu().numpy(), fc=b.fc.cpu().numpy(), ex=ex)
 
 
-@pytest.fixture(scope="module", params=SCEN)
+_CACHE = {}
+
+
+def _cached(name, int_mode):
+    key = (name, int_mode)
+    if key not in _CACHE:
+        d = F.load(name)
+        _CACHE[key] = _solve(d, d["records"], int_mode)
+    return _CACHE[key]
+
+
+# "round" is the default direct MILP path (thermal DP + exact battery LP); "round_lp" solves
+# the relaxation first (ADMM + polish) and then runs the same integer DP
+@pytest.fixture(scope="module", params=[(s, m) for s in SCEN for m in ("round", "round_lp")],
+                ids=lambda p: f"{p[0]}-{p[1]}")
 def solved(request, gpu):
-    d = F.load(request.param)
-    recs = d["records"]
-    return request.param, d, recs, _solve(d, recs, "relax"), _solve(d, recs, "round")
+    name, mode = request.param
+    d = F.load(name)
+    return name, d, d["records"], _cached(name, "relax"), _cached(name, mode)
 
 
 def test_lp_status_and_objective(solved):
@@ -203,3 +217,23 @@ def test_success_fields_match(solved):
         assert ours["correct_solve"] == 1 and ours["solve_counter"] == 0
         for j in range(len(r["draw_size"]) - 1):
             assert ours[f"waterdraws_{j}"] == r["optimal_vals"][f"waterdraws_{j}"]
+
+
+def test_battery_lp_exact(solved):
+    """The MILP is separable, so the battery part of any optimum is an optimum of the battery
+    LP alone.  The direct path's piecewise-linear DP must reach the same battery cost
+    sum_k gamma^k price_k S (ch_k + dis_k) as the relaxation's certified vertex."""
+    from dragg_amd import _lib as L
+    name, d, recs, rel, rnd = solved
+    ich, idis = L.FC_KEYS.index("p_batt_ch"), L.FC_KEYS.index("p_batt_disch")
+    n = 0
+    for i, r in enumerate(recs):
+        if rel["status"][i] != L.ST_OPTIMAL or rnd["status"][i] != L.ST_OPTIMAL or r["E0"] is None:
+            continue
+        H = rel["fc"].shape[1]
+        w = 0.92 ** np.arange(H) * np.array(r["total_price"][:H]) * 6
+        c_rel = float(w @ (rel["fc"][ich, :, i] + rel["fc"][idis, :, i]))
+        c_rnd = float(w @ (rnd["fc"][ich, :, i] + rnd["fc"][idis, :, i]))
+        assert abs(c_rel - c_rnd) <= 1e-9 * max(1.0, abs(c_rel)), (name, i, c_rel, c_rnd)
+        n += 1
+    print(f"{name}: battery LP cost identical on {n} records")
