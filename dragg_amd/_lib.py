@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libdragg_mi355x.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # enums (mirror include/dragg_mi355x.h)
 BASE, PV_ONLY, BATTERY_ONLY, PV_BATTERY = 0, 1, 2, 3
@@ -52,7 +52,7 @@ class Dims(ctypes.Structure):
 class Problem(ctypes.Structure):
     _fields_ = [("params", c_dp), ("home_type", c_dp), ("draw_hourly", c_dp), ("oat", c_dp), ("ghi", c_dp),
                 ("tou", c_dp), ("reward_price", c_dp), ("start_index", ctypes.c_int32),
-                ("home_offset", ctypes.c_int32), ("seed", ctypes.c_uint64)]
+                ("home_offset", ctypes.c_int32), ("seed", ctypes.c_uint64), ("workspace", c_dp)]
 
 
 class Hash(ctypes.Structure):
@@ -69,7 +69,8 @@ class Explicit(ctypes.Structure):
                 ("draw", c_dp), ("oat", c_dp), ("ghi", c_dp), ("price", c_dp)]
 
 
-EXPORTS = ["dragg_mpc_abi_version", "dragg_mpc_strerror", "dragg_mpc_lds_bytes", "dragg_mpc_step",
+EXPORTS = ["dragg_mpc_abi_version", "dragg_mpc_strerror", "dragg_mpc_lds_bytes", "dragg_mpc_workspace_bytes",
+           "dragg_mpc_step",
            "dragg_mpc_solve_explicit", "dragg_mpc_aggregate", "dragg_mpc_season_noise"]
 
 _LIB = None
@@ -92,6 +93,8 @@ def load(path=LIB_PATH):
     lib.dragg_mpc_strerror.restype = ctypes.c_char_p
     lib.dragg_mpc_strerror.argtypes = [ctypes.c_int]
     lib.dragg_mpc_lds_bytes.argtypes = [ctypes.POINTER(Dims)]
+    lib.dragg_mpc_workspace_bytes.argtypes = [ctypes.POINTER(Dims)]
+    lib.dragg_mpc_workspace_bytes.restype = ctypes.c_int64
     lib.dragg_mpc_step.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Problem), ctypes.POINTER(Hash),
                                    ctypes.POINTER(Out), ctypes.c_int32, c_dp, c_dp]
     lib.dragg_mpc_solve_explicit.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Problem),

@@ -1309,30 +1309,39 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
 // No relaxation / ADMM is needed on this path; the LP kernel above remains the solver of
 // the relaxation (int_mode relax) and of the relaxation-then-round variant (round_lp).
 // ======================================================================================
-constexpr int NB_CAP = 384;          // DP bins per chain (natural count at dt = 4 is <= ~330)
+constexpr int NB_CAP = 352;          // DP buckets per chain (config ranges need <= ~330 at any dt)
+constexpr int NBND = 8;              // box-boundary buckets per stage (dp_zspace; 4-5 in practice)
 
 struct LdsD {
     double *draw, *oat, *ghi, *price;   // [H+1]
     double *x;                          // [8H] solution in the stage-slot layout of the LP path
     double *t2;                         // [H] p_grid (objective)
     double *cA, *cC, *cq;               // [H] coefficients of the chain being solved
-    double *bx0, *bp1, *bp2;            // [H] battery: merged-domain origin, psi segment offsets
-    double *sgS, *sgL;                  // [2][seg_cap] battery segments (slope, length)
-    double2 *lab0, *lab1;               // [NB_CAP] DP labels (cost, exact state), 2 buffers
+    double *rt;                         // [H+2] zero-duty reference trajectory of the chain
     double *sc;                         // [32] scalars / reduction scratch
-    double *rt;                         // [H+1] zero-duty reference trajectory of the chain
-    int *tarr, *inv;                    // [NB_CAP], [NB_CAP+8] DP source keys / inverse table
-    uint16_t* par;                      // [H][NB_CAP] DP back-pointers
+    double *bx0, *bp1, *bp2;            // [H] battery: merged-domain origin, psi segment offsets
+    double2 *lab;                       // [NB_CAP] DP labels (cost, exact state)
+    double2 *rmin;                      // [NB_CAP+8] DP cheapest source label per key
+                                        //   (dp_fixed: its second label buffer)
+    double2 *cand;                      // [NBND][S+1] boundary-bucket candidates per duty
+    int *tarr, *rsrc, *candp;           // [NB_CAP], [NB_CAP+8], [NBND][S+1] keys, rmin source, records
+    double *sgS, *sgL;                  // battery segments [2][seg_cap], in lab / rmin (the
+                                        //   battery LP runs after the thermal DPs)
+    uint16_t* par;                      // [H][NB_CAP] DP back-pointers (global workspace)
 };
 
 __host__ __device__ inline int seg_cap(int H) { return ((2 * H + 2 + 63) / 64) * 64; }
 
-__host__ __device__ inline int direct_lds_bytes(int H) {
-    const int nd = 4 * (H + 1) + 8 * H + H + 3 * H + 3 * H + 4 * seg_cap(H) + 4 * NB_CAP + 32 + (H + 2) + 1;
-    return nd * 8 + (2 * NB_CAP + 8) * 4 + ((H * NB_CAP * 2 + 15) / 16) * 16;
+// the battery segment lists must fit in the DP label arrays they reuse
+__host__ __device__ inline bool direct_fits(int H) { return seg_cap(H) <= NB_CAP; }
+
+__host__ __device__ inline int direct_lds_bytes(int H, int S) {
+    const int nd = 4 * (H + 1) + 8 * H + H + 3 * H + (H + 2) + 32 + 3 * H + 1 + 2 * NB_CAP + 2 * (NB_CAP + 8) +
+                   2 * NBND * (S + 1);
+    return nd * 8 + (NB_CAP + NB_CAP + 8 + NBND * (S + 1)) * 4;
 }
 
-DEV LdsD carve_direct(double* s, int H) {
+DEV LdsD carve_direct(double* s, int H, int S) {
     LdsD L;
     double* const base = s;
     L.draw = s; s += H + 1;
@@ -1344,20 +1353,21 @@ DEV LdsD carve_direct(double* s, int H) {
     L.cA = s; s += H;
     L.cC = s; s += H;
     L.cq = s; s += H;
+    L.rt = s; s += H + 2;
+    L.sc = s; s += 32;
     L.bx0 = s; s += H;
     L.bp1 = s; s += H;
     L.bp2 = s; s += H;
-    const int sc = seg_cap(H);
-    L.sgS = s; s += 2 * sc;
-    L.sgL = s; s += 2 * sc;
     if ((s - base) & 1) ++s;                                     // 16-B alignment of the labels
-    L.lab0 = reinterpret_cast<double2*>(s); s += 2 * NB_CAP;
-    L.lab1 = reinterpret_cast<double2*>(s); s += 2 * NB_CAP;
-    L.sc = s; s += 32;
-    L.rt = s; s += H + 2;
+    L.lab = reinterpret_cast<double2*>(s); s += 2 * NB_CAP;
+    L.rmin = reinterpret_cast<double2*>(s); s += 2 * (NB_CAP + 8);
+    L.cand = reinterpret_cast<double2*>(s); s += 2 * NBND * (S + 1);
     L.tarr = reinterpret_cast<int*>(s);
-    L.inv = L.tarr + NB_CAP;
-    L.par = reinterpret_cast<uint16_t*>(L.inv + NB_CAP + 8);
+    L.rsrc = L.tarr + NB_CAP;
+    L.candp = L.rsrc + NB_CAP + 8;
+    L.sgS = reinterpret_cast<double*>(L.lab);
+    L.sgL = reinterpret_cast<double*>(L.rmin);
+    L.par = nullptr;                                             // set by the kernel
     return L;
 }
 
@@ -1440,8 +1450,8 @@ DEV bool dp_fixed(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
     const int S = SS > 0 ? SS : h.S;
     const DpGeom G = dp_geom(fmin(lo0, lo), fmax(hi0, hi), g);
     const int nb = G.nb;
-    double2* cur = L.lab0;
-    double2* nxt = L.lab1;
+    double2* cur = L.lab;
+    double2* nxt = L.rmin;
     const double BIG = INFINITY;
     for (int k = 0; k < H; ++k) {
         const double Ak = L.cA[k], Ck = L.cC[k], ck = L.cq[k];
@@ -1466,29 +1476,6 @@ DEV bool dp_fixed(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
             if (k == 0) {
                 for (int u = 0; u <= S; ++u)
                     consider(fma(Ak, x0, fma(g, (double)u, Ck)), ck * u, u);
-            } else if (SS > 0 && ncand == 3) {
-                // all loads first (one 16-B label per candidate), then branch-free selects
-                double2 lv[NU][3];
-                double base[NU];
-                int s0[NU];
-#pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    base[u] = fma(g, (double)u, Ck);
-                    s0[u] = dp_first_source(G, B, iA, base[u]);
-#pragma unroll
-                    for (int d = 0; d < 3; ++d) {
-                        const int sb = min(max(s0[u] + d, 0), nb - 1);
-                        lv[u][d] = cur[sb];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < NU; ++u)
-#pragma unroll
-                    for (int d = 0; d < 3; ++d) {
-                        const int sb = s0[u] + d;
-                        const double cs = (sb >= 0 && sb < nb) ? lv[u][d].x : BIG;
-                        consider(fma(Ak, lv[u][d].y, base[u]), fma(ck, (double)u, cs), u | (d << 4));
-                    }
             } else {
                 for (int u = 0; u <= S; ++u) {
                     const double bs = fma(g, (double)u, Ck);
@@ -1566,8 +1553,11 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
     constexpr int NU = SS > 0 ? SS + 1 : 16;
     const int H = h.H;
     const int S = SS > 0 ? SS : h.S;
-    const double w = fabs(g) / NBU, iw = 1.0 / w;
-    const int sh = g > 0.0 ? NBU : -NBU;
+    // buckets per duty unit: NBU at 15-min steps, proportionally more at coarser steps so that
+    // the bucket width (in degrees) does not grow with the step length
+    const int nbu = max(NBU, (4 * NBU) / max(1, h.dt));
+    const double w = fabs(g) / nbu, iw = 1.0 / w;
+    const int sh = g > 0.0 ? nbu : -nbu;
     const double BIG = INFINITY;
     {
         const double tl = lo - TOL_P * (1 + fabs(lo)), th = hi + TOL_P * (1 + fabs(hi));
@@ -1590,8 +1580,7 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         *blo = (int)floor((tl - r) * iw + c1) - 1;
         return (int)floor((th - r) * iw + c1) + 1 - *blo + 1;
     };
-    double2* cur = L.lab0;
-    double2* nxt = L.lab1;
+    double2* lab = L.lab;
     // stage 0: from the single initial label (z = 1/2) to buckets sh*u + floor(A_0 / 2) = sh*u
     double c = 0.5;
     double cn1 = L.cA[0] * c;
@@ -1600,13 +1589,13 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
     {
         const double A0 = L.cA[0], C0 = L.cC[0], q0 = L.cq[0];
         const double tl = lo0 - TOL_P * (1 + fabs(lo0)), th = hi0 + TOL_P * (1 + fabs(hi0));
-        for (int j = lane; j < nbz; j += nt) { cur[j] = make_double2(BIG, 0.0); L.par[j] = 0xFFFF; }
+        for (int j = lane; j < nbz; j += nt) { lab[j] = make_double2(BIG, 0.0); L.par[j] = 0xFFFF; }
         __syncthreads();
         for (int u = lane; u <= S; u += nt) {
             const int j = sh * u + (int)floor(cn1) - blo;
             const double xn = fma(A0, x0, fma(g, (double)u, C0));
             if (j >= 0 && j < nbz && xn >= tl && xn <= th) {
-                cur[j] = make_double2(q0 * u, xn);
+                lab[j] = make_double2(q0 * u, xn);
                 L.par[j] = (uint16_t)(u << 12);
             }
         }
@@ -1620,81 +1609,135 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         // (a) source keys T_s = floor(A_k z_s), z clamped into the bucket (keeps T monotone);
         //     an empty bucket uses its centre
         for (int s = lane; s < nbz; s += nt) {
-            const double2 lv = cur[s];
+            const double2 lv = lab[s];
             const double b = (double)(blo + s);
             double zz = lv.x < BIG ? (lv.y - rk) * iw + c : b + 0.5;
             zz = fmin(fmax(zz, b), b + 0.999999);
             L.tarr[s] = (int)floor(Ak * zz);
         }
         __syncthreads();
-        // (b) inverse table: inv[m - mlo] = first source with T >= m, inv[mhi - mlo + 1] = nbz
-        const int mlo = L.tarr[0], mhi = L.tarr[nbz - 1];
-        for (int s = lane; s < nbz; s += nt) {
-            const int T = L.tarr[s];
-            const int Tp = s > 0 ? L.tarr[s - 1] : mlo - 1;
-            for (int m = Tp + 1; m <= T; ++m) L.inv[m - mlo] = s;
-            if (s == nbz - 1) L.inv[mhi - mlo + 1] = nbz;
-        }
-        __syncthreads();
-        // (c) targets
+        // target window of stage k+1 and its box-boundary buckets: a bucket strictly inside the
+        // box (margin far above rounding) accepts every label landing in it, so only a run's
+        // cheapest label can win there; the 4-5 boundary buckets need every run member with
+        // the exact box test.
         const double c1 = Ak * c;
         int blo1;
         const int nbz1 = window(k, c1, &blo1);
-        for (int j = lane; j < nbz1; j += nt) {
-            const int b = blo1 + j;
-            double best = BIG, bx = 0.0;
-            int bp = 0xFFFF;
-            auto consider = [&](double2 lv, double base, int u, int src) {
-                const double xn = fma(Ak, lv.y, base);
-                const double cn = fma(ck, (double)u, lv.x);
-                const bool ok = (xn >= tl) & (xn <= th) & (cn < best);
-                best = ok ? cn : best;
-                bx = ok ? xn : bx;
-                bp = ok ? (src | (u << 12)) : bp;
-            };
-            if constexpr (SS > 0) {
-                int sa[NU], sb[NU];
-#pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    const int m = b - sh * u;
-                    const bool in = m >= mlo && m <= mhi;
-                    const int mi = in ? m - mlo : 0;
-                    sa[u] = in ? L.inv[mi] : 0;
-                    sb[u] = in ? L.inv[mi + 1] : 0;
+        const double r1 = L.rt[k + 1];
+        int jin0 = (int)ceil((tl - r1) * iw + c1 + 1e-6) - blo1;
+        int jin1 = (int)floor((th - r1) * iw + c1 - 1e-6) - 1 - blo1;
+        jin0 = min(max(jin0, 0), nbz1);
+        jin1 = min(max(jin1, jin0 - 1), nbz1 - 1);
+        const int nleft = jin0, nbnd = jin0 + (nbz1 - 1 - jin1);
+        if (nbnd > NBND) return -1;                       // degenerate box: caller uses dp_fixed
+        auto bidx = [&](int j) { return j < nleft ? j : j - jin1 - 1 + nleft; };   // boundary j -> q
+        struct Best { double c, x; int p; };
+        auto consider = [&](Best& B, double2 lv, double base, int u, int src) {
+            const double xn = fma(Ak, lv.y, base);
+            const double cn = fma(ck, (double)u, lv.x);
+            const bool ok = (xn >= tl) & (xn <= th) & (cn < B.c);
+            B.c = ok ? cn : B.c;
+            B.x = ok ? xn : B.x;
+            B.p = ok ? (src | (u << 12)) : B.p;
+        };
+        // (b) per key m: the cheapest label of the run {s : T_s = m} (ascending s, first minimum)
+        //     and its bucket, at index m - mlo + 1 (keys skipped by the contraction: rsrc = -1;
+        //     indices 0 and M + 2 are empty sentinels, so a clamped index needs no range test);
+        //     the run's owner also resolves the boundary buckets it reaches (one (bucket, duty)
+        //     pair per key: no write conflicts) into cand
+        const int mlo = L.tarr[0], mhi = L.tarr[nbz - 1], M = mhi - mlo;
+        if (lane == 0) {
+            L.rmin[0] = make_double2(BIG, 0.0); L.rsrc[0] = -1;
+            L.rmin[M + 2] = make_double2(BIG, 0.0); L.rsrc[M + 2] = -1;
+        }
+        const int reach_lo = min(0, sh * S), reach_hi = max(0, sh * S);
+        const int bl0 = blo1, bl1 = blo1 + jin0 - 1, br0 = blo1 + jin1 + 1, br1 = blo1 + nbz1 - 1;
+        for (int s = lane; s < nbz; s += nt) {
+            const int T = L.tarr[s];
+            const int Tp = s > 0 ? L.tarr[s - 1] : mlo - 1;
+            for (int m = Tp + 1; m < T; ++m) { L.rmin[m - mlo + 1] = make_double2(BIG, 0.0); L.rsrc[m - mlo + 1] = -1; }
+            if (T > Tp) {
+                double2 bl = lab[s];
+                int bs = s, s2 = s + 1;
+                for (; s2 < nbz && L.tarr[s2] == T; ++s2) {
+                    const double2 lv = lab[s2];
+                    if (lv.x < bl.x) { bl = lv; bs = s2; }
                 }
-                double2 l0[NU], l1[NU];
-#pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    l0[u] = cur[min(sa[u], nbz - 1)];
-                    l1[u] = cur[min(sa[u] + 1, nbz - 1)];
-                }
-#pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    const double base = fma(g, (double)u, Ck);
-                    if (sa[u] < sb[u]) consider(l0[u], base, u, sa[u]);
-                    if (sa[u] + 1 < sb[u]) consider(l1[u], base, u, sa[u] + 1);
-                    for (int s2 = sa[u] + 2; s2 < sb[u]; ++s2) consider(cur[s2], base, u, s2);
-                }
-            } else {
-                for (int u = 0; u <= S; ++u) {
-                    const int m = b - sh * u;
-                    if (m < mlo || m > mhi) continue;
-                    const double base = fma(g, (double)u, Ck);
-                    for (int s2 = L.inv[m - mlo]; s2 < L.inv[m - mlo + 1]; ++s2) consider(cur[s2], base, u, s2);
+                L.rmin[T - mlo + 1] = bl;
+                L.rsrc[T - mlo + 1] = bs;
+                const int r0 = T + reach_lo, r1 = T + reach_hi;
+                if ((r0 <= bl1 && r1 >= bl0) || (r0 <= br1 && r1 >= br0)) {
+                    for (int u = 0; u <= S; ++u) {
+                        const int j = T + sh * u - blo1;
+                        if (j < 0 || j >= nbz1 || (j >= jin0 && j <= jin1)) continue;
+                        Best B{BIG, 0.0, 0xFFFF};
+                        const double base = fma(g, (double)u, Ck);
+                        for (int s3 = s; s3 < s2; ++s3) consider(B, lab[s3], base, u, s3);
+                        const int ci = bidx(j) * (S + 1) + u;
+                        L.cand[ci] = make_double2(B.c, B.x);
+                        L.candp[ci] = B.p;
+                    }
                 }
             }
-            nxt[j] = make_double2(best, bx);
-            L.par[k * NB_CAP + j] = (uint16_t)bp;
         }
         __syncthreads();
-        double2* t = cur; cur = nxt; nxt = t;
+        // (c) targets, written over the label array in place (nothing here reads it).  Interior
+        //     buckets: the first (in duty order) cheapest run minimum; the box test is implied.
+        for (int j = lane; j < nbz1; j += nt) {
+            const int b = blo1 + j;
+            Best B{BIG, 0.0, 0xFFFF};
+            if (j >= jin0 && j <= jin1) {
+                const int m0 = b - mlo + 1;
+                double bc = BIG;
+                int bu = -1, bmi = 0;
+                if constexpr (SS > 0) {
+                    double2 lv[NU];
+                    int mi[NU];
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) {
+                        mi[u] = min(max(m0 - sh * u, 0), M + 2);
+                        lv[u] = L.rmin[mi[u]];
+                    }
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) {
+                        const double cn = fma(ck, (double)u, lv[u].x);
+                        const bool ok = cn < bc;
+                        bc = ok ? cn : bc;
+                        bu = ok ? u : bu;
+                        bmi = ok ? mi[u] : bmi;
+                    }
+                } else {
+                    for (int u = 0; u <= S; ++u) {
+                        const int mu = min(max(m0 - sh * u, 0), M + 2);
+                        const double cn = fma(ck, (double)u, L.rmin[mu].x);
+                        if (cn < bc) { bc = cn; bu = u; bmi = mu; }
+                    }
+                }
+                if (bu >= 0) {
+                    B.c = bc;
+                    B.x = fma(Ak, L.rmin[bmi].y, fma(g, (double)bu, Ck));
+                    B.p = L.rsrc[bmi] | (bu << 12);
+                }
+            } else {
+                const int q = bidx(j);
+                for (int u = 0; u <= S; ++u) {
+                    const int m = b - sh * u;
+                    if (m < mlo || m > mhi || L.rsrc[m - mlo + 1] < 0) continue;
+                    const double2 cv = L.cand[q * (S + 1) + u];
+                    if (cv.x < B.c) { B.c = cv.x; B.x = cv.y; B.p = L.candp[q * (S + 1) + u]; }
+                }
+            }
+            lab[j] = make_double2(B.c, B.x);
+            L.par[k * NB_CAP + j] = (uint16_t)B.p;
+        }
+        __syncthreads();
         blo = blo1; nbz = nbz1; c = c1;
     }
     // cheapest final label (lowest bucket on ties, deterministic)
     double best = BIG;
     int bb = -1;
     for (int j = lane; j < nbz; j += nt)
-        if (cur[j].x < best) { best = cur[j].x; bb = j; }
+        if (lab[j].x < best) { best = lab[j].x; bb = j; }
     for (int o = 32; o > 0; o >>= 1) {
         const double ob = __shfl_xor(best, o);
         const int oi = __shfl_xor(bb, o);
@@ -1875,7 +1918,8 @@ __global__ __launch_bounds__(NT) void mpc_direct_kernel(KArgs a) {
     if (home >= N) return;
     Home h;
     const int H = a.d.horizon;
-    LdsD D = carve_direct(smem, H);
+    LdsD D = carve_direct(smem, H, a.d.sub_steps);
+    D.par = reinterpret_cast<uint16_t*>(a.p.workspace) + (size_t)home * H * NB_CAP;
     Lds L = lp_view(D);
     Io io{a.vals, a.fc, N, home};
     Prof pf;
@@ -1990,14 +2034,19 @@ __global__ void noise_kernel(int N, int H, uint64_t seed, int off, int t, double
 
 bool direct_mode(const dragg_mpc_dims* d) { return d->int_mode == DRAGG_INT_ROUND; }
 
+size_t workspace_bytes(const dragg_mpc_dims* d) {
+    return direct_mode(d) ? (size_t)d->n_homes * d->horizon * NB_CAP * sizeof(uint16_t) : 0;
+}
+
 size_t kernel_lds_bytes(const dragg_mpc_dims* d) {
-    return direct_mode(d) ? (size_t)direct_lds_bytes(d->horizon) : (size_t)lds_doubles(d->horizon) * 8;
+    return direct_mode(d) ? (size_t)direct_lds_bytes(d->horizon, d->sub_steps) : (size_t)lds_doubles(d->horizon) * 8;
 }
 
 int check_dims(const dragg_mpc_dims* d) {
     if (!d || d->n_homes < 0 || d->horizon < 1 || d->sub_steps < 1 || d->dt < 1) return DRAGG_E_ARG;
     if (d->int_mode < DRAGG_INT_ROUND || d->int_mode > DRAGG_INT_ROUND_LP) return DRAGG_E_ARG;
     if (direct_mode(d) && d->sub_steps > 15) return DRAGG_E_ARG;     // 4-bit duty in the DP record
+    if (direct_mode(d) && !direct_fits(d->horizon)) return DRAGG_E_HORIZON;
     if (kernel_lds_bytes(d) > 160 * 1024) return DRAGG_E_HORIZON;
     return DRAGG_OK;
 }
@@ -2054,6 +2103,12 @@ const char* dragg_mpc_strerror(int code) {
     }
 }
 
+int64_t dragg_mpc_workspace_bytes(const dragg_mpc_dims* dims) {
+    const int rc = check_dims(dims);
+    if (rc) return rc;
+    return (int64_t)workspace_bytes(dims);
+}
+
 int dragg_mpc_lds_bytes(const dragg_mpc_dims* dims) {
     const int rc = check_dims(dims);
     if (rc) return rc;
@@ -2070,6 +2125,7 @@ int dragg_mpc_step(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob, dr
         return DRAGG_E_ARG;
     if (dims->n_rp != 1 && dims->n_rp < dims->horizon) return DRAGG_E_ARG;   // numpy broadcast error
     if (prob->start_index + timestep + dims->horizon >= dims->n_env) return DRAGG_E_ARG;
+    if (direct_mode(dims) && !prob->workspace) return DRAGG_E_ARG;
     KArgs a{};
     a.d = *dims; a.p = *prob; a.vals = hash->vals; a.fc = hash->fc; a.out = *out; a.noise = noise;
     a.t = timestep;
@@ -2086,6 +2142,7 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
         !in->price || !hash->vals || !hash->fc || !out->status || !out->iters || !out->obj ||
         !out->relax_obj)
         return DRAGG_E_ARG;
+    if (direct_mode(dims) && !prob->workspace) return DRAGG_E_ARG;
     KArgs a{};
     a.d = *dims; a.p = *prob; a.ex = *in; a.vals = hash->vals; a.fc = hash->fc; a.out = *out;
     return launch<true>(a, (hipStream_t)stream);

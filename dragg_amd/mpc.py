@@ -135,6 +135,10 @@ class MPCBatch:
         if rc < 0:
             L.check(rc)
         self.lds_bytes = rc
+        ws = self.lib.dragg_mpc_workspace_bytes(ctypes.byref(self.dims))
+        if ws < 0:
+            L.check(int(ws))
+        self.workspace = torch.empty(max(1, (ws + 7) // 8), dtype=torch.int64, device=dev) if ws > 0 else None
 
     # ------------------------------------------------------------------ environment
     def set_environment(self, oat, ghi, tou, start_index):
@@ -159,7 +163,7 @@ class MPCBatch:
         return L.Problem(params=L.ptr(self.params), home_type=L.ptr(self.types), draw_hourly=L.ptr(self.draws),
                          oat=L.ptr(self.oat), ghi=L.ptr(self.ghi), tou=L.ptr(self.tou),
                          reward_price=L.ptr(self.rp), start_index=self.start_index,
-                         home_offset=self.home_offset, seed=self.seed)
+                         home_offset=self.home_offset, seed=self.seed, workspace=L.ptr(self.workspace))
 
     def _hash(self):
         return L.Hash(vals=L.ptr(self.vals), fc=L.ptr(self.fc))

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DRAGG_MPC_ABI_VERSION 2
+#define DRAGG_MPC_ABI_VERSION 3
 
 /* home types (aggregator.py:425, 468, 520, 555); bit 0 = pv, bit 1 = battery */
 enum dragg_home_type {
@@ -131,6 +131,9 @@ typedef struct dragg_mpc_problem {
     int32_t start_index;        /* start_hour_index (aggregator.py:630-638)             */
     int32_t home_offset;        /* global index of home 0 of this shard (noise key)     */
     uint64_t seed;              /* keyed season-noise stream when noise == NULL         */
+    void* workspace;            /* device scratch, dragg_mpc_workspace_bytes(dims) bytes */
+                                /* (int_mode round: DP back-pointers); may be NULL when  */
+                                /* that size is 0                                        */
 } dragg_mpc_problem;
 
 typedef struct dragg_mpc_hash {
@@ -179,6 +182,9 @@ const char* dragg_mpc_strerror(int code);
 
 /* Dynamic LDS bytes one home (workgroup) needs for this horizon; < 0 if H unsupported. */
 int dragg_mpc_lds_bytes(const dragg_mpc_dims* dims);
+
+/* Device workspace bytes a launch with these dims needs (problem.workspace); < 0 on error. */
+int64_t dragg_mpc_workspace_bytes(const dragg_mpc_dims* dims);
 
 /* One closed-loop timestep for all N homes: reads the hash arrays (t > 0) or the
    parameters (t == 0), solves, and writes the hash arrays back in place.

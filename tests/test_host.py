@@ -142,3 +142,24 @@ def test_reward_price_length_rule():
     with pytest.raises(ValueError):
         MPCBatch.set_reward_price(type("B", (), {"H": 24, "device": "cpu", "dims": type("D", (), {})()})(),
                                   [0.0] * 4)
+
+
+def test_size_queries_without_gpu(lib_path):
+    """dragg_mpc_lds_bytes / dragg_mpc_workspace_bytes are host-only queries (no GPU needed)."""
+    from dragg_amd import _lib as L
+    lib = L.load()
+    d = L.Dims(n_homes=100, horizon=24, sub_steps=6, dt=4, n_draw_hours=48, n_env=0, n_rp=1,
+               int_mode=L.INT_ROUND, max_iter=0, check_every=0, discount=0.92)
+    ws = lib.dragg_mpc_workspace_bytes(ctypes.byref(d))
+    assert ws % (100 * 24 * 2) == 0 and ws // (100 * 24 * 2) >= 330   # uint16 per bucket and stage
+    lds_direct = lib.dragg_mpc_lds_bytes(ctypes.byref(d))
+    assert 0 < lds_direct <= 20 * 1024                 # 8 homes per CU at H = 24
+    d.int_mode = L.INT_RELAX
+    assert lib.dragg_mpc_workspace_bytes(ctypes.byref(d)) == 0
+    assert lib.dragg_mpc_lds_bytes(ctypes.byref(d)) > lds_direct
+    d.int_mode = 7
+    assert lib.dragg_mpc_workspace_bytes(ctypes.byref(d)) < 0
+    d.int_mode = L.INT_ROUND
+    d.horizon = 400                                    # LP kernel's LDS is the binding limit
+    d.int_mode = L.INT_RELAX
+    assert lib.dragg_mpc_lds_bytes(ctypes.byref(d)) == -4
