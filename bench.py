@@ -1,20 +1,25 @@
 #!/usr/bin/env python3
 """Benchmark: home-MPC solves/sec (homes x timesteps) of the batched MI355X solver.
 
-Workload (BASELINE.json configs[1]): 1,000 homes (40 % base,
-20 % pv_only, 20 % battery_only, 20 % pv_battery), run_rbo_mpc closed loop at 15-min
-steps (dt = 4), 6 h horizon (H = 24), S = 6, discount 0.92, TOU prices; synthetic
-NSRDB-shaped January weather and synthetic homes (no network for the reference data).
-A "step" is one closed-loop timestep of the whole community: one launch of the
-batched solver (every home's MPC solve + state advance) plus the aggregate reduction
-(and, with N > 1 GPUs, the 24-byte RCCL all-reduce).  Homes shard across ranks
-(weak scaling: --homes is per GPU).
+Workload (BASELINE.json configs[2], the configuration its metric is quoted on, "at 10k
+homes"): a 10,000-home community (40 % base, 20 % pv_only, 20 % battery_only, 20 %
+pv_battery), run_rbo_mpc closed loop at 15-min steps (dt = 4) with a 12 h horizon (H = 48),
+S = 6, discount 0.92, TOU prices, int_mode round (the reference's MILP).  Inputs are
+synthetic: NSRDB-shaped July weather (Houston-like) and homes drawn from the config.toml
+ranges (no network for the reference data).  July, because with the reference's season
+draw (1.1^k-scaled OAT noise, mpc_calc.py:222, 303-309) a 12 h horizon in January sends
+nearly every home to the cooling-only mode and the fallback thermostat (tests/golden/c3_h48:
+96/96), which would benchmark the fallback, not the solver; `--month 1` runs it anyway.
 
-Default: warmup 4 timesteps, then 96 timed timesteps (the full 24 h day) on 1 GPU.
+A "step" is one closed-loop timestep of the whole community: one solver launch per rank
+(every home's MPC solve + state advance), the aggregate reduction and, with N > 1 GPUs, the
+24-byte RCCL all-reduce.  The community is sharded over the ranks (strong scaling: --homes
+is the community size).  `value` = homes x timed steps / max-over-ranks wall time.
 
-Also reported (rank 0, N = 1 only): `cpu_baseline`, the repo's CPU restatement of the
-reference solve (oracle/, HiGHS MILP in place of GLPK_MI) timed on this host's cores
-on a bounded sample of the same workload, and `roofline` for the solver kernel.
+Also reported (rank 0): `roofline` of the solver kernel (algorithmic HBM bytes per launch
+over the launch time measured with HIP events on the launch stream), `cpu_baseline` (N = 1
+only): the repo's CPU restatement of the reference solve (oracle/, HiGHS MILP in place of
+GLPK_MI) timed on this host's cores on a bounded sample of the same workload.
 """
 import argparse
 import json
@@ -32,9 +37,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=96)
     ap.add_argument("--warmup", type=int, default=4)
-    ap.add_argument("--homes", type=int, default=1000, help="homes per GPU")
-    ap.add_argument("--horizon-hours", type=int, default=6)
+    ap.add_argument("--homes", type=int, default=10000, help="community size (sharded over the ranks)")
+    ap.add_argument("--horizon-hours", type=int, default=12)
     ap.add_argument("--dt", type=int, default=4)
+    ap.add_argument("--month", type=int, default=7, choices=[1, 4, 7, 10])
     ap.add_argument("--int-mode", default="round", choices=["round", "relax", "round_lp"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--cpu-workers", type=int, default=0)
@@ -89,17 +95,38 @@ def cpu_baseline(homes, env, seconds, workers):
 
 
 # ----------------------------------------------------------------------------- roofline
-def bytes_per_step(batch, success_frac):
-    """Algorithmic HBM bytes of one solver launch."""
+def bytes_per_launch(batch, success_frac):
+    """Algorithmic HBM bytes of one solver launch: per home the parameters,
+    type, the hourly draw rows of the window and the hash state read; the hash fields,
+    status/objective outputs and (on success) the forecast fields written."""
     import numpy as np
     H, dt = batch.H, batch.dt
     types = batch.types_host
     n = len(types)
-    rd = n * (22 * 8 + 4 + (H // dt + 1) * 8 + 6 * 8)            # params, type, draw window, hash state
+    rd = n * (22 * 8 + 4 + ((H + 1) // dt + 2) * 8 + 6 * 8)
     nfc = 10 + 2 * ((types & 1) != 0) + 3 * ((types & 2) != 0)   # forecast keys per home type
     wr = n * (19 * 8 + 4 + 4 + 8 + 8) + success_frac * float(np.sum(nfc)) * H * 8
     env = 3 * (H + 1) * 8
     return rd + wr + env
+
+
+def measured_traffic(workload_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes of this workload
+    (profiles/*/traffic.json: FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                tj = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if tj.get("workload") == workload_key:
+            return tj.get("bytes_per_launch"), os.path.relpath(f, ROOT)
+    return None, None
+
+
+def traffic_key(n_total, H, dt, month, int_mode, world):
+    return f"{n_total} homes, H={H}, dt={dt}, month {month}, int_mode={int_mode}, {world} rank(s)"
 
 
 def main():
@@ -112,9 +139,9 @@ def main():
     total_steps = args.warmup + args.steps
     sim_hours = math.ceil(total_steps / dt)
     days = math.ceil((sim_hours + Hh + 2) / 24) + 1
-    n_total = args.homes * world
+    n_total = args.homes
     homes = synthetic_homes(n_total, seed=12, days=days, dt=dt, horizon_hours=Hh)
-    oat, ghi, tou = synthetic_weather(days, dt, sim_hours, seed=3)
+    oat, ghi, tou = synthetic_weather(days, dt, sim_hours, seed=3, month=args.month)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -161,29 +188,30 @@ def main():
     solves = n_total * args.steps
     value = solves / elapsed
     if rank == 0:
-        achieved = bytes_per_step(agg.batch, success) / (kern_ms * 1e-3) / 1e9
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(tf):
-            with open(tf) as f:
-                tj = json.load(f)
-            if tj.get("homes") == args.homes and tj.get("horizon") == agg.batch.H:
-                traffic = tj.get("bytes_per_launch")
+        H = agg.batch.H
+        workload = (f"{n_total} homes x {args.steps} closed-loop {60 // dt}-min steps, H={H} "
+                    f"({Hh} h), month {args.month}, run_rbo_mpc, int_mode={args.int_mode}")
+        achieved = bytes_per_launch(agg.batch, success) / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = measured_traffic(traffic_key(n_total, H, dt, args.month, args.int_mode, world))
         out = {
             "metric": "home-MPC solves/sec (homes x steps)", "value": value, "unit": "solves/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64", "data": "synthetic (NSRDB-shaped weather, config.toml-range homes)",
-            "config": {"workload": f"{args.homes} homes/GPU x {args.steps} closed-loop 15-min steps, "
-                                   f"H={agg.batch.H} (6 h), run_rbo_mpc, int_mode={args.int_mode}",
-                       "homes_total": n_total, "global_batch": n_total, "horizon": agg.batch.H,
-                       "mix": "40/20/20/20 base/pv/battery/pv_battery", "parallelism": f"homes sharded x{world}"},
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (NSRDB-shaped weather, config.toml-range homes, seeded)",
+            "config": {"workload": workload, "baseline_config": "BASELINE.json configs[2]",
+                       "homes_total": n_total, "homes_per_gpu": agg.batch.N, "global_batch": n_total,
+                       "horizon": H, "mix": "40/20/20/20 base/pv/battery/pv_battery",
+                       "parallelism": f"homes sharded x{world}"},
+            "sim_wall_s": elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                         "frac": achieved / 8000.0, "traffic": traffic,
-                         "kernel": "mpc_home_kernel<false>", "kernel_ms": kern_ms},
+                         "frac": achieved / 8000.0,
+                         "traffic": (traffic / (kern_ms * 1e-3) / 1e9) if traffic else None,
+                         "traffic_bytes_per_launch": traffic, "traffic_source": traffic_src,
+                         "kernel": f"mpc_{'direct' if args.int_mode == 'round' else 'home'}_kernel",
+                         "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
             "status_counts": stat_counts,
-            "mean_admm_iters": float(agg.batch.iters.float().mean()),
         }
         print(json.dumps(out))
     if world > 1:

@@ -173,3 +173,51 @@ def test_collected_aggregates(scen):
     for t, vals in by_t.items():
         if len(vals) == len(homes):
             assert abs(sum(vals) - agg[t]) <= 1e-9 * max(1.0, abs(agg[t])), (name, t)
+
+
+def _battery_lp(hc, si):
+    """The battery block alone (mpc_calc.py:355-373 with its cost term S*(ch+dis), :405-432):
+    min sum_k gamma^k price_k S (ch_k + dis_k), E_k = E0 + sum_{j<k} (eta_c ch_j + dis_j/eta_d)/dt."""
+    from scipy.optimize import linprog
+    H, S, dt, b = hc.H, hc.S, hc.dt, hc.batt
+    w = np.power(hc.discount * np.ones(H), np.arange(H)) * np.asarray(si.price[:H], float) * S
+    low = np.tril(np.ones((H, H)))
+    A = np.hstack([low * (b["eta_c"] / dt), low * ((1.0 / b["eta_d"]) / dt)])
+    res = linprog(np.r_[w, w], A_ub=np.vstack([A, -A]),
+                  b_ub=np.r_[np.full(H, b["Emax"] - si.E0), np.full(H, si.E0 - b["Emin"])],
+                  bounds=[(0, b["rate"])] * H + [(-b["rate"], 0)] * H, method="highs")
+    assert res.status == 0
+    return res.fun
+
+
+def _pv_part(hc, si):
+    """The PV block alone (mpc_calc.py:375-385): curtail (u = 1) only where the weight is < 0."""
+    H, S = hc.H, hc.S
+    w = np.power(hc.discount * np.ones(H), np.arange(H)) * np.asarray(si.price[:H], float) * S
+    p = hc.pv["area"] * hc.pv["eff"] * np.asarray(si.ghi[:H], float) / 1000
+    return float(np.sum(np.where(w < 0, 0.0, -w * p)))
+
+
+def test_model_is_separable(scen):
+    """The default GPU path rests on the model being separable: the
+    reference's LP (and MILP) optimum = thermal part (the model of a 'base' home) + battery
+    LP + PV LP.  Checked against the reference's recorded objectives."""
+    import dataclasses
+    name, d, homes = scen
+    recs = [r for r in d["records"] if r["lp_status"] == 0 and r["type"] != "base"]
+    recs = recs[::max(1, len(recs) // 60)]
+    n_lp = n_milp = 0
+    for r in recs:
+        hc = M.home_const(homes[r["name"]])
+        si = _si(r)
+        base = dataclasses.replace(hc, type="base")
+        st, _, thermal = M.solve_problem(M.build_problem(base, si), integer=False)
+        assert st == "optimal"
+        rest = (_battery_lp(hc, si) if hc.has_batt else 0.0) + (_pv_part(hc, si) if hc.has_pv else 0.0)
+        assert abs(thermal + rest - r["lp_obj"]) <= 1e-7 * max(1.0, abs(r["lp_obj"])), (name, r["name"], r["t"])
+        n_lp += 1
+        if hc.H <= 12 and r["status"] == "optimal" and r["milp_obj"] is not None and (r["milp_gap"] or 0) < 1e-6:
+            st, _, thermal_i = M.solve_problem(M.build_problem(base, si), integer=True, time_limit=20.0)
+            assert abs(thermal_i + rest - r["milp_obj"]) <= 1e-6 * max(1.0, abs(r["milp_obj"])), (name, r["name"])
+            n_milp += 1
+    print(f"{name}: separable on {n_lp} LP and {n_milp} MILP records")

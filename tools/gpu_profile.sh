@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/prof
 mkdir -p $OUT
-ARGS=${@:-"--homes 10000 --steps 6 --warmup 1 --cpu-seconds 0"}
+ARGS=${@:-"--homes 10000 --horizon-hours 12 --month 7 --steps 6 --warmup 1 --cpu-seconds 0"}
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_available.txt 2>&1 || true
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || exit 1
 pass() {
