@@ -1630,7 +1630,6 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         jin1 = min(max(jin1, jin0 - 1), nbz1 - 1);
         const int nleft = jin0, nbnd = jin0 + (nbz1 - 1 - jin1);
         if (nbnd > NBND) return -1;                       // degenerate box: caller uses dp_fixed
-        auto bidx = [&](int j) { return j < nleft ? j : j - jin1 - 1 + nleft; };   // boundary j -> q
         struct Best { double c, x; int p; };
         auto consider = [&](Best& B, double2 lv, double base, int u, int src) {
             const double xn = fma(Ak, lv.y, base);
@@ -1650,8 +1649,7 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
             L.rmin[0] = make_double2(BIG, 0.0); L.rsrc[0] = -1;
             L.rmin[M + 2] = make_double2(BIG, 0.0); L.rsrc[M + 2] = -1;
         }
-        const int reach_lo = min(0, sh * S), reach_hi = max(0, sh * S);
-        const int bl0 = blo1, bl1 = blo1 + jin0 - 1, br0 = blo1 + jin1 + 1, br1 = blo1 + nbz1 - 1;
+        const double iA = 1.0 / Ak;
         for (int s = lane; s < nbz; s += nt) {
             const int T = L.tarr[s];
             const int Tp = s > 0 ? L.tarr[s - 1] : mlo - 1;
@@ -1665,67 +1663,72 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
                 }
                 L.rmin[T - mlo + 1] = bl;
                 L.rsrc[T - mlo + 1] = bs;
-                const int r0 = T + reach_lo, r1 = T + reach_hi;
-                if ((r0 <= bl1 && r1 >= bl0) || (r0 <= br1 && r1 >= br0)) {
-                    for (int u = 0; u <= S; ++u) {
-                        const int j = T + sh * u - blo1;
-                        if (j < 0 || j >= nbz1 || (j >= jin0 && j <= jin1)) continue;
-                        Best B{BIG, 0.0, 0xFFFF};
-                        const double base = fma(g, (double)u, Ck);
-                        for (int s3 = s; s3 < s2; ++s3) consider(B, lab[s3], base, u, s3);
-                        const int ci = bidx(j) * (S + 1) + u;
-                        L.cand[ci] = make_double2(B.c, B.x);
-                        L.candp[ci] = B.p;
-                    }
-                }
             }
+        }
+        // boundary (bucket q, duty u) pairs, one per lane: the run of key m = b - sh*u is
+        // located from the near-linear key map (T_s ~ A s) and walked to, then every member is
+        // tested against the exact box
+        for (int idx = lane; idx < nbnd * (S + 1); idx += nt) {
+            const int q = idx / (S + 1), u = idx - q * (S + 1);
+            const int j = q < nleft ? q : jin1 + 1 + (q - nleft);
+            const int m = blo1 + j - sh * u;
+            Best B{BIG, 0.0, 0xFFFF};
+            if (m >= mlo && m <= mhi) {
+                int s0 = min(max((int)((m - mlo) * iA), 0), nbz - 1);
+                while (s0 < nbz - 1 && L.tarr[s0] < m) ++s0;
+                while (s0 > 0 && L.tarr[s0 - 1] >= m) --s0;
+                const double base = fma(g, (double)u, Ck);
+                for (int s3 = s0; s3 < nbz && L.tarr[s3] == m; ++s3) consider(B, lab[s3], base, u, s3);
+            }
+            L.cand[idx] = make_double2(B.c, B.x);
+            L.candp[idx] = B.p;
         }
         __syncthreads();
         // (c) targets, written over the label array in place (nothing here reads it).  Interior
         //     buckets: the first (in duty order) cheapest run minimum; the box test is implied.
-        for (int j = lane; j < nbz1; j += nt) {
-            const int b = blo1 + j;
-            Best B{BIG, 0.0, 0xFFFF};
-            if (j >= jin0 && j <= jin1) {
-                const int m0 = b - mlo + 1;
-                double bc = BIG;
-                int bu = -1, bmi = 0;
-                if constexpr (SS > 0) {
-                    double2 lv[NU];
-                    int mi[NU];
+        for (int j = jin0 + lane; j <= jin1; j += nt) {
+            const int m0 = blo1 + j - mlo + 1;
+            double bc = BIG;
+            int bu = -1, bmi = 0;
+            if constexpr (SS > 0) {
+                double2 lv[NU];
+                int mi[NU];
 #pragma unroll
-                    for (int u = 0; u < NU; ++u) {
-                        mi[u] = min(max(m0 - sh * u, 0), M + 2);
-                        lv[u] = L.rmin[mi[u]];
-                    }
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) {
-                        const double cn = fma(ck, (double)u, lv[u].x);
-                        const bool ok = cn < bc;
-                        bc = ok ? cn : bc;
-                        bu = ok ? u : bu;
-                        bmi = ok ? mi[u] : bmi;
-                    }
-                } else {
-                    for (int u = 0; u <= S; ++u) {
-                        const int mu = min(max(m0 - sh * u, 0), M + 2);
-                        const double cn = fma(ck, (double)u, L.rmin[mu].x);
-                        if (cn < bc) { bc = cn; bu = u; bmi = mu; }
-                    }
+                for (int u = 0; u < NU; ++u) {
+                    mi[u] = min(max(m0 - sh * u, 0), M + 2);
+                    lv[u] = L.rmin[mi[u]];
                 }
-                if (bu >= 0) {
-                    B.c = bc;
-                    B.x = fma(Ak, L.rmin[bmi].y, fma(g, (double)bu, Ck));
-                    B.p = L.rsrc[bmi] | (bu << 12);
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const double cn = fma(ck, (double)u, lv[u].x);
+                    const bool ok = cn < bc;
+                    bc = ok ? cn : bc;
+                    bu = ok ? u : bu;
+                    bmi = ok ? mi[u] : bmi;
                 }
             } else {
-                const int q = bidx(j);
                 for (int u = 0; u <= S; ++u) {
-                    const int m = b - sh * u;
-                    if (m < mlo || m > mhi || L.rsrc[m - mlo + 1] < 0) continue;
-                    const double2 cv = L.cand[q * (S + 1) + u];
-                    if (cv.x < B.c) { B.c = cv.x; B.x = cv.y; B.p = L.candp[q * (S + 1) + u]; }
+                    const int mu = min(max(m0 - sh * u, 0), M + 2);
+                    const double cn = fma(ck, (double)u, L.rmin[mu].x);
+                    if (cn < bc) { bc = cn; bu = u; bmi = mu; }
                 }
+            }
+            double2 out = make_double2(BIG, 0.0);
+            int p = 0xFFFF;
+            if (bu >= 0) {
+                out = make_double2(bc, fma(Ak, L.rmin[bmi].y, fma(g, (double)bu, Ck)));
+                p = L.rsrc[bmi] | (bu << 12);
+            }
+            lab[j] = out;
+            L.par[k * NB_CAP + j] = (uint16_t)p;
+        }
+        // boundary buckets: the first cheapest of their per-duty candidates
+        for (int q = lane; q < nbnd; q += nt) {
+            const int j = q < nleft ? q : jin1 + 1 + (q - nleft);
+            Best B{BIG, 0.0, 0xFFFF};
+            for (int u = 0; u <= S; ++u) {
+                const double2 cv = L.cand[q * (S + 1) + u];
+                if (cv.x < B.c) { B.c = cv.x; B.x = cv.y; B.p = L.candp[q * (S + 1) + u]; }
             }
             lab[j] = make_double2(B.c, B.x);
             L.par[k * NB_CAP + j] = (uint16_t)B.p;
@@ -1910,7 +1913,7 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
 }
 
 template <bool EXPLICIT, int NT>
-__global__ __launch_bounds__(NT) void mpc_direct_kernel(KArgs a) {
+__global__ __launch_bounds__(NT, 2) void mpc_direct_kernel(KArgs a) {   // 2 waves/SIMD: 8 homes per CU
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int home = blockIdx.x;
     const int lane = threadIdx.x;
@@ -1945,29 +1948,33 @@ __global__ __launch_bounds__(NT) void mpc_direct_kernel(KArgs a) {
     pf.mark(DRAGG_PH_SETUP);
     double obj = NAN;
     if (status == DRAGG_ST_OPTIMAL) {
-        // indoor air chain (mpc_calc.py:314-317); u = duty of the season's mode (:303-309)
-        for (int k = lane; k < H; k += NT) {
-            D.cA[k] = h.aT;
-            D.cC[k] = D.oat[k + 1] * h.iR * 3600 * h.inv_c;
-            D.cq[k] = pow(h.gamma, (double)k) * D.price[k] * h.Pact;
-            D.x[k * 8 + S_PAD] = 0.0;
-            D.x[k * 8 + S_CH] = 0.0; D.x[k * 8 + S_DIS] = 0.0; D.x[k * 8 + S_E] = 0.0;
-        }
-        __syncthreads();
-        bool ok;
-        if (h.S == 6) ok = dp_thermal<6>(h, D, lane, NT, h.g, h.T0, h.Tmin, h.Tmax, h.Tmin, h.Tmax, S_T, S_U);
-        else ok = dp_thermal<0>(h, D, lane, NT, h.g, h.T0, h.Tmin, h.Tmax, h.Tmin, h.Tmax, S_T, S_U);
-        // water-heater chain given T (mpc_calc.py:330-332)
-        if (ok) {
+        // chain 0: indoor air (mpc_calc.py:314-317), u = duty of the season's mode (:303-309);
+        // chain 1: water heater given T (mpc_calc.py:330-332).  One DP instantiation for both.
+        bool ok = true;
+        for (int chain = 0; chain < 2 && ok; ++chain) {
             for (int k = lane; k < H; k += NT) {
-                const double df = D.draw[k + 1] / h.V, rem = 1 - df, d15 = df * TAP;
-                D.cA[k] = rem + (-rem * h.iRw) * 3600 * h.inv_w;
-                D.cC[k] = h.e * D.x[k * 8 + S_T] + (d15 + ((-d15) * h.iRw) * 3600 * h.inv_w);
-                D.cq[k] = pow(h.gamma, (double)k) * D.price[k] * (h.S * h.Pw);
+                const double wk = pow(h.gamma, (double)k) * D.price[k];
+                if (chain == 0) {
+                    D.cA[k] = h.aT;
+                    D.cC[k] = D.oat[k + 1] * h.iR * 3600 * h.inv_c;
+                    D.cq[k] = wk * h.Pact;
+                    D.x[k * 8 + S_PAD] = 0.0;
+                    D.x[k * 8 + S_CH] = 0.0; D.x[k * 8 + S_DIS] = 0.0; D.x[k * 8 + S_E] = 0.0;
+                } else {
+                    const double df = D.draw[k + 1] / h.V, rem = 1 - df, d15 = df * TAP;
+                    D.cA[k] = rem + (-rem * h.iRw) * 3600 * h.inv_w;
+                    D.cC[k] = h.e * D.x[k * 8 + S_T] + (d15 + ((-d15) * h.iRw) * 3600 * h.inv_w);
+                    D.cq[k] = wk * (h.S * h.Pw);
+                }
             }
             __syncthreads();
-            if (h.S == 6) ok = dp_thermal<6>(h, D, lane, NT, h.f, h.Tw0, twlo0, twhi0, h.Twmin, h.Twmax, S_TW, S_W);
-            else ok = dp_thermal<0>(h, D, lane, NT, h.f, h.Tw0, twlo0, twhi0, h.Twmin, h.Twmax, S_TW, S_W);
+            const bool c0 = chain == 0;
+            const double g = c0 ? h.g : h.f, x0 = c0 ? h.T0 : h.Tw0;
+            const double lo0 = c0 ? h.Tmin : twlo0, hi0 = c0 ? h.Tmax : twhi0;
+            const double lo = c0 ? h.Tmin : h.Twmin, hi = c0 ? h.Tmax : h.Twmax;
+            const int sx = c0 ? S_T : S_TW, sv = c0 ? S_U : S_W;
+            ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
+                          : dp_thermal<0>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
         }
         pf.mark(DRAGG_PH_INTEGER);
         if (!ok) status = DRAGG_ST_ROUND_FAIL;
