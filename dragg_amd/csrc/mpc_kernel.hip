@@ -1309,7 +1309,7 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
 // No relaxation / ADMM is needed on this path; the LP kernel above remains the solver of
 // the relaxation (int_mode relax) and of the relaxation-then-round variant (round_lp).
 // ======================================================================================
-constexpr int NB_CAP = 352;          // DP buckets per chain (config ranges need <= ~330 at any dt)
+constexpr int NB_CAP = 336;          // DP buckets per chain (config ranges need <= ~327 at any dt)
 constexpr int NBND = 8;              // box-boundary buckets per stage (dp_zspace; 4-5 in practice)
 
 struct LdsD {
@@ -1324,7 +1324,8 @@ struct LdsD {
     double2 *rmin;                      // [NB_CAP+8] DP cheapest source label per key
                                         //   (dp_fixed: its second label buffer)
     double2 *cand;                      // [NBND][S+1] boundary-bucket candidates per duty
-    int *tarr, *rsrc, *candp;           // [NB_CAP], [NB_CAP+8], [NBND][S+1] keys, rmin source, records
+    int16_t *tarr, *rsrc;               // [NB_CAP], [NB_CAP+8] source keys, source of rmin
+    int *candp;                         // [NBND][S+1] candidate records
     double *sgS, *sgL;                  // battery segments [2][seg_cap], in lab / rmin (the
                                         //   battery LP runs after the thermal DPs)
     uint16_t* par;                      // [H][NB_CAP] DP back-pointers (global workspace)
@@ -1332,41 +1333,56 @@ struct LdsD {
 
 __host__ __device__ inline int seg_cap(int H) { return ((2 * H + 2 + 63) / 64) * 64; }
 
-// the battery segment lists must fit in the DP label arrays they reuse
+// The battery LP runs after the thermal DPs: its segment lists live in lab (sgS) and rmin
+// (sgL); for H up to ~60 its recovery arrays (bx0, bp1, bp2) also fit in lab and the
+// objective's p_grid (t2) in rmin ("compact" layout), else they get arrays of their own.
+__host__ __device__ inline bool direct_compact(int H) {
+    return 2 * seg_cap(H) + 3 * H <= 2 * NB_CAP && 2 * seg_cap(H) + H <= 2 * (NB_CAP + 8);
+}
 __host__ __device__ inline bool direct_fits(int H) { return seg_cap(H) <= NB_CAP; }
 
 __host__ __device__ inline int direct_lds_bytes(int H, int S) {
-    const int nd = 4 * (H + 1) + 8 * H + H + 3 * H + (H + 2) + 32 + 3 * H + 1 + 2 * NB_CAP + 2 * (NB_CAP + 8) +
-                   2 * NBND * (S + 1);
-    return nd * 8 + (NB_CAP + NB_CAP + 8 + NBND * (S + 1)) * 4;
+    int nd = 4 * (H + 1) + 8 * H + 3 * H + (H + 2) + 32 + 1 + 2 * NB_CAP + 2 * (NB_CAP + 8) + 2 * NBND * (S + 1);
+    if (!direct_compact(H)) nd += 4 * H;
+    return nd * 8 + (NB_CAP + NB_CAP + 8) * 2 + NBND * (S + 1) * 4;
 }
 
 DEV LdsD carve_direct(double* s, int H, int S) {
     LdsD L;
     double* const base = s;
+    const bool compact = direct_compact(H);
     L.draw = s; s += H + 1;
     L.oat = s; s += H + 1;
     L.ghi = s; s += H + 1;
     L.price = s; s += H + 1;
     L.x = s; s += 8 * H;
-    L.t2 = s; s += H;
     L.cA = s; s += H;
     L.cC = s; s += H;
     L.cq = s; s += H;
     L.rt = s; s += H + 2;
     L.sc = s; s += 32;
-    L.bx0 = s; s += H;
-    L.bp1 = s; s += H;
-    L.bp2 = s; s += H;
+    if (!compact) {
+        L.t2 = s; s += H;
+        L.bx0 = s; s += H;
+        L.bp1 = s; s += H;
+        L.bp2 = s; s += H;
+    }
     if ((s - base) & 1) ++s;                                     // 16-B alignment of the labels
     L.lab = reinterpret_cast<double2*>(s); s += 2 * NB_CAP;
     L.rmin = reinterpret_cast<double2*>(s); s += 2 * (NB_CAP + 8);
     L.cand = reinterpret_cast<double2*>(s); s += 2 * NBND * (S + 1);
-    L.tarr = reinterpret_cast<int*>(s);
+    L.tarr = reinterpret_cast<int16_t*>(s);
     L.rsrc = L.tarr + NB_CAP;
-    L.candp = L.rsrc + NB_CAP + 8;
+    L.candp = reinterpret_cast<int*>(L.rsrc + NB_CAP + 8);
+    const int sc = seg_cap(H);
     L.sgS = reinterpret_cast<double*>(L.lab);
     L.sgL = reinterpret_cast<double*>(L.rmin);
+    if (compact) {
+        L.bx0 = L.sgS + 2 * sc;
+        L.bp1 = L.bx0 + H;
+        L.bp2 = L.bp1 + H;
+        L.t2 = L.sgL + 2 * sc;
+    }
     L.par = nullptr;                                             // set by the kernel
     return L;
 }
@@ -1563,6 +1579,7 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         const double tl = lo - TOL_P * (1 + fabs(lo)), th = hi + TOL_P * (1 + fabs(hi));
         if ((th - tl) * iw + 4.0 > (double)NB_CAP) return -1;
     }
+    const double zspan = 30000.0;                                 // int16 keys and sources
     if (lane == 0) {
         double r = x0;
         L.rt[0] = r;
@@ -1581,6 +1598,10 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         return (int)floor((th - r) * iw + c1) + 1 - *blo + 1;
     };
     double2* lab = L.lab;
+    for (int k = 0; k <= H; ++k) {                                // keys must fit in int16
+        const double zr = fmax(fabs((lo - L.rt[k]) * iw), fabs((hi - L.rt[k]) * iw));
+        if (!(zr < zspan)) return -1;
+    }
     // stage 0: from the single initial label (z = 1/2) to buckets sh*u + floor(A_0 / 2) = sh*u
     double c = 0.5;
     double cn1 = L.cA[0] * c;
@@ -1613,7 +1634,7 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
             const double b = (double)(blo + s);
             double zz = lv.x < BIG ? (lv.y - rk) * iw + c : b + 0.5;
             zz = fmin(fmax(zz, b), b + 0.999999);
-            L.tarr[s] = (int)floor(Ak * zz);
+            L.tarr[s] = (int16_t)floor(Ak * zz);
         }
         __syncthreads();
         // target window of stage k+1 and its box-boundary buckets: a bucket strictly inside the
@@ -1662,7 +1683,7 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
                     if (lv.x < bl.x) { bl = lv; bs = s2; }
                 }
                 L.rmin[T - mlo + 1] = bl;
-                L.rsrc[T - mlo + 1] = bs;
+                L.rsrc[T - mlo + 1] = (int16_t)bs;
             }
         }
         // boundary (bucket q, duty u) pairs, one per lane: the run of key m = b - sh*u is
