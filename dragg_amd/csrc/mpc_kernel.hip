@@ -1623,20 +1623,21 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         __syncthreads();
     }
     c = cn1;
+    // source key of a label for the next stage: T = floor(A z), z clamped into its bucket
+    // (keeps T monotone in the bucket index); an empty bucket uses its centre
+    auto key = [&](double2 lv, int b, double A, double r, double cz) -> int16_t {
+        const double fb = (double)b;
+        double zz = lv.x < BIG ? (lv.y - r) * iw + cz : fb + 0.5;
+        zz = fmin(fmax(zz, fb), fb + 0.999999);
+        return (int16_t)floor(A * zz);
+    };
+    if (H > 1) {
+        for (int s = lane; s < nbz; s += nt) L.tarr[s] = key(lab[s], blo + s, L.cA[1], L.rt[1], c);
+        __syncthreads();
+    }
     for (int k = 1; k < H; ++k) {
         const double Ak = L.cA[k], Ck = L.cC[k], ck = L.cq[k];
         const double tl = lo - TOL_P * (1 + fabs(lo)), th = hi + TOL_P * (1 + fabs(hi));
-        const double rk = L.rt[k];
-        // (a) source keys T_s = floor(A_k z_s), z clamped into the bucket (keeps T monotone);
-        //     an empty bucket uses its centre
-        for (int s = lane; s < nbz; s += nt) {
-            const double2 lv = lab[s];
-            const double b = (double)(blo + s);
-            double zz = lv.x < BIG ? (lv.y - rk) * iw + c : b + 0.5;
-            zz = fmin(fmax(zz, b), b + 0.999999);
-            L.tarr[s] = (int16_t)floor(Ak * zz);
-        }
-        __syncthreads();
         // target window of stage k+1 and its box-boundary buckets: a bucket strictly inside the
         // box (margin far above rounding) accepts every label landing in it, so only a run's
         // cheapest label can win there; the 4-5 boundary buckets need every run member with
@@ -1662,9 +1663,8 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         };
         // (b) per key m: the cheapest label of the run {s : T_s = m} (ascending s, first minimum)
         //     and its bucket, at index m - mlo + 1 (keys skipped by the contraction: rsrc = -1;
-        //     indices 0 and M + 2 are empty sentinels, so a clamped index needs no range test);
-        //     the run's owner also resolves the boundary buckets it reaches (one (bucket, duty)
-        //     pair per key: no write conflicts) into cand
+        //     indices 0 and M + 2 are empty sentinels, so a clamped index needs no range test).
+        //     Runs are 1-2 buckets while A_k > 2/3: both members are loaded up front.
         const int mlo = L.tarr[0], mhi = L.tarr[nbz - 1], M = mhi - mlo;
         if (lane == 0) {
             L.rmin[0] = make_double2(BIG, 0.0); L.rsrc[0] = -1;
@@ -1674,13 +1674,19 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         for (int s = lane; s < nbz; s += nt) {
             const int T = L.tarr[s];
             const int Tp = s > 0 ? L.tarr[s - 1] : mlo - 1;
+            const int Tn = s + 1 < nbz ? L.tarr[s + 1] : mhi + 1;
+            const double2 l0 = lab[s];
+            const double2 l1 = lab[min(s + 1, nbz - 1)];
             for (int m = Tp + 1; m < T; ++m) { L.rmin[m - mlo + 1] = make_double2(BIG, 0.0); L.rsrc[m - mlo + 1] = -1; }
             if (T > Tp) {
-                double2 bl = lab[s];
-                int bs = s, s2 = s + 1;
-                for (; s2 < nbz && L.tarr[s2] == T; ++s2) {
-                    const double2 lv = lab[s2];
-                    if (lv.x < bl.x) { bl = lv; bs = s2; }
+                double2 bl = l0;
+                int bs = s;
+                if (Tn == T) {
+                    if (l1.x < bl.x) { bl = l1; bs = s + 1; }
+                    for (int s2 = s + 2; s2 < nbz && L.tarr[s2] == T; ++s2) {
+                        const double2 lv = lab[s2];
+                        if (lv.x < bl.x) { bl = lv; bs = s2; }
+                    }
                 }
                 L.rmin[T - mlo + 1] = bl;
                 L.rsrc[T - mlo + 1] = (int16_t)bs;
@@ -1705,43 +1711,51 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
             L.candp[idx] = B.p;
         }
         __syncthreads();
-        // (c) targets, written over the label array in place (nothing here reads it).  Interior
-        //     buckets: the first (in duty order) cheapest run minimum; the box test is implied.
+        // (c) targets, written over the label array in place (nothing here reads it or the
+        //     keys), each with its key for the next stage.  Interior buckets: the first (in duty
+        //     order) cheapest run minimum, with its state and source carried along; the box test
+        //     is implied.
+        const bool more = k + 1 < H;
+        const double An = more ? L.cA[k + 1] : 1.0;
         for (int j = jin0 + lane; j <= jin1; j += nt) {
             const int m0 = blo1 + j - mlo + 1;
-            double bc = BIG;
-            int bu = -1, bmi = 0;
+            double bc = BIG, bxs = 0.0;
+            int bu = -1, bsr = 0;
             if constexpr (SS > 0) {
                 double2 lv[NU];
-                int mi[NU];
+                int sr[NU];
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
-                    mi[u] = min(max(m0 - sh * u, 0), M + 2);
-                    lv[u] = L.rmin[mi[u]];
+                    const int mi = min(max(m0 - sh * u, 0), M + 2);
+                    lv[u] = L.rmin[mi];
+                    sr[u] = L.rsrc[mi];
                 }
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
                     const double cn = fma(ck, (double)u, lv[u].x);
                     const bool ok = cn < bc;
                     bc = ok ? cn : bc;
+                    bxs = ok ? lv[u].y : bxs;
+                    bsr = ok ? sr[u] : bsr;
                     bu = ok ? u : bu;
-                    bmi = ok ? mi[u] : bmi;
                 }
             } else {
                 for (int u = 0; u <= S; ++u) {
                     const int mu = min(max(m0 - sh * u, 0), M + 2);
-                    const double cn = fma(ck, (double)u, L.rmin[mu].x);
-                    if (cn < bc) { bc = cn; bu = u; bmi = mu; }
+                    const double2 lv = L.rmin[mu];
+                    const double cn = fma(ck, (double)u, lv.x);
+                    if (cn < bc) { bc = cn; bxs = lv.y; bsr = L.rsrc[mu]; bu = u; }
                 }
             }
             double2 out = make_double2(BIG, 0.0);
             int p = 0xFFFF;
             if (bu >= 0) {
-                out = make_double2(bc, fma(Ak, L.rmin[bmi].y, fma(g, (double)bu, Ck)));
-                p = L.rsrc[bmi] | (bu << 12);
+                out = make_double2(bc, fma(Ak, bxs, fma(g, (double)bu, Ck)));
+                p = bsr | (bu << 12);
             }
             lab[j] = out;
             L.par[k * NB_CAP + j] = (uint16_t)p;
+            if (more) L.tarr[j] = key(out, blo1 + j, An, r1, c1);
         }
         // boundary buckets: the first cheapest of their per-duty candidates
         for (int q = lane; q < nbnd; q += nt) {
@@ -1751,8 +1765,10 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
                 const double2 cv = L.cand[q * (S + 1) + u];
                 if (cv.x < B.c) { B.c = cv.x; B.x = cv.y; B.p = L.candp[q * (S + 1) + u]; }
             }
-            lab[j] = make_double2(B.c, B.x);
+            const double2 out = make_double2(B.c, B.x);
+            lab[j] = out;
             L.par[k * NB_CAP + j] = (uint16_t)B.p;
+            if (more) L.tarr[j] = key(out, blo1 + j, An, r1, c1);
         }
         __syncthreads();
         blo = blo1; nbz = nbz1; c = c1;
