@@ -1719,39 +1719,38 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         const double An = more ? L.cA[k + 1] : 1.0;
         for (int j = jin0 + lane; j <= jin1; j += nt) {
             const int m0 = blo1 + j - mlo + 1;
-            double bc = BIG, bxs = 0.0;
-            int bu = -1, bsr = 0;
+            double bc = BIG;
+            int bu = -1;
             if constexpr (SS > 0) {
                 double2 lv[NU];
-                int sr[NU];
+                // keys of all duties inside [0, M+2] (most interior buckets): no clamping
+                const bool inside = min(m0, m0 - sh * SS) >= 0 && max(m0, m0 - sh * SS) <= M + 2;
+                if (inside) {
 #pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    const int mi = min(max(m0 - sh * u, 0), M + 2);
-                    lv[u] = L.rmin[mi];
-                    sr[u] = L.rsrc[mi];
+                    for (int u = 0; u < NU; ++u) lv[u] = L.rmin[m0 - sh * u];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) lv[u] = L.rmin[min(max(m0 - sh * u, 0), M + 2)];
                 }
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
                     const double cn = fma(ck, (double)u, lv[u].x);
                     const bool ok = cn < bc;
                     bc = ok ? cn : bc;
-                    bxs = ok ? lv[u].y : bxs;
-                    bsr = ok ? sr[u] : bsr;
                     bu = ok ? u : bu;
                 }
             } else {
                 for (int u = 0; u <= S; ++u) {
-                    const int mu = min(max(m0 - sh * u, 0), M + 2);
-                    const double2 lv = L.rmin[mu];
-                    const double cn = fma(ck, (double)u, lv.x);
-                    if (cn < bc) { bc = cn; bxs = lv.y; bsr = L.rsrc[mu]; bu = u; }
+                    const double cn = fma(ck, (double)u, L.rmin[min(max(m0 - sh * u, 0), M + 2)].x);
+                    if (cn < bc) { bc = cn; bu = u; }
                 }
             }
             double2 out = make_double2(BIG, 0.0);
             int p = 0xFFFF;
-            if (bu >= 0) {
-                out = make_double2(bc, fma(Ak, bxs, fma(g, (double)bu, Ck)));
-                p = bsr | (bu << 12);
+            if (bu >= 0) {                 // the winner's state and source
+                const int mi = min(max(m0 - sh * bu, 0), M + 2);
+                out = make_double2(bc, fma(Ak, L.rmin[mi].y, fma(g, (double)bu, Ck)));
+                p = L.rsrc[mi] | (bu << 12);
             }
             lab[j] = out;
             L.par[k * NB_CAP + j] = (uint16_t)p;
