@@ -51,6 +51,14 @@ SCENARIOS = {
     # then raises KeyError('e_batt_opt') at t=1, mpc_calc.py:285)
     "spring_dt1": dict(n=8, batt=2, pv=2, pvb=2, start="2015-04-02 00", end="2015-04-03 00",
                        dt=1, horizon=4, action_horizon=4, seed=5, record_t=range(0, 24)),
+    # negative total prices (an RL reward price, broadcast through the redis 'reward_price'
+    # list as aggregator.py:671-675 does): battery charge-while-discharge edge, PV curtailment
+    "negprice_dt1": dict(n=8, batt=2, pv=2, pvb=2, start="2015-04-02 00", end="2015-04-03 00",
+                         dt=1, horizon=4, action_horizon=4, seed=11, record_t=range(0, 24),
+                         rp=[-0.12, 0.03, -0.2, 0.0]),
+    "negprice_dt2": dict(n=4, batt=1, pv=1, pvb=1, start="2015-01-01 00", end="2015-01-01 12",
+                         dt=2, horizon=6, action_horizon=6, seed=13, record_t=range(0, 24),
+                         rp=[round(0.11 * np.sin(0.5 * k) - 0.04, 4) for k in range(12)]),
 }
 
 CONFIG_TMPL = """
@@ -248,6 +256,16 @@ def run(name, sc, hook=None):
     mc.MPCCalc.cleanup_and_finish = cleanup
 
     agg = ag.Aggregator()
+    if sc.get("rp") is not None:            # the RL agent's reward-price broadcast, fixed
+        orig_init = agg.redis_set_initial_values
+
+        def init_vals():
+            orig_init()
+            agg.reward_price = np.array(sc["rp"], dtype=float)
+            agg.redis_client.conn.delete("reward_price")
+            agg.redis_client.conn.rpush("reward_price", *agg.reward_price.tolist())
+
+        agg.redis_set_initial_values = init_vals
     orig_create = agg.create_homes
 
     def create_homes():
