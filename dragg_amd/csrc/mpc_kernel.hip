@@ -1701,11 +1701,28 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
             const int m = blo1 + j - sh * u;
             Best B{BIG, 0.0, 0xFFFF};
             if (m >= mlo && m <= mhi) {
-                int s0 = min(max((int)((m - mlo) * iA), 0), nbz - 1);
-                while (s0 < nbz - 1 && L.tarr[s0] < m) ++s0;
-                while (s0 > 0 && L.tarr[s0 - 1] >= m) --s0;
+                // T_s = floor(A z), z in [b, b+1): a member's bucket b lies in
+                // (m/A - 1, (m+1)/A); one bucket of margin each side covers rounding
+                const int sa = max((int)floor(m * iA) - 2 - blo, 0);
+                const int sb = min((int)floor((m + 1) * iA) + 1 - blo, nbz - 1);
                 const double base = fma(g, (double)u, Ck);
-                for (int s3 = s0; s3 < nbz && L.tarr[s3] == m; ++s3) consider(B, lab[s3], base, u, s3);
+                constexpr int W = 6;
+                if (sb - sa < W) {
+                    int tk[W];
+                    double2 lv[W];
+#pragma unroll
+                    for (int i = 0; i < W; ++i) {
+                        const int s3 = min(sa + i, sb);
+                        tk[i] = L.tarr[s3];
+                        lv[i] = lab[s3];
+                    }
+#pragma unroll
+                    for (int i = 0; i < W; ++i)
+                        if (sa + i <= sb && tk[i] == m) consider(B, lv[i], base, u, sa + i);
+                } else {
+                    for (int s3 = sa; s3 <= sb; ++s3)
+                        if (L.tarr[s3] == m) consider(B, lab[s3], base, u, s3);
+                }
             }
             L.cand[idx] = make_double2(B.c, B.x);
             L.candp[idx] = B.p;
@@ -1717,24 +1734,25 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         //     is implied.
         const bool more = k + 1 < H;
         const double An = more ? L.cA[k + 1] : 1.0;
-        for (int j = jin0 + lane; j <= jin1; j += nt) {
+        // the first (in duty order) cheapest run minimum of target j (SS > 0: keys of all
+        // duties inside [0, M+2] for most interior buckets, no clamping)
+        auto pick = [&](int j, double& bc, int& bu) {
             const int m0 = blo1 + j - mlo + 1;
-            double bc = BIG;
-            int bu = -1;
+            bc = BIG;
+            bu = -1;
             if constexpr (SS > 0) {
-                double2 lv[NU];
-                // keys of all duties inside [0, M+2] (most interior buckets): no clamping
+                double lv[NU];
                 const bool inside = min(m0, m0 - sh * SS) >= 0 && max(m0, m0 - sh * SS) <= M + 2;
                 if (inside) {
 #pragma unroll
-                    for (int u = 0; u < NU; ++u) lv[u] = L.rmin[m0 - sh * u];
+                    for (int u = 0; u < NU; ++u) lv[u] = L.rmin[m0 - sh * u].x;
                 } else {
 #pragma unroll
-                    for (int u = 0; u < NU; ++u) lv[u] = L.rmin[min(max(m0 - sh * u, 0), M + 2)];
+                    for (int u = 0; u < NU; ++u) lv[u] = L.rmin[min(max(m0 - sh * u, 0), M + 2)].x;
                 }
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
-                    const double cn = fma(ck, (double)u, lv[u].x);
+                    const double cn = fma(ck, (double)u, lv[u]);
                     const bool ok = cn < bc;
                     bc = ok ? cn : bc;
                     bu = ok ? u : bu;
@@ -1745,24 +1763,53 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
                     if (cn < bc) { bc = cn; bu = u; }
                 }
             }
+        };
+        // run-minimum index of the winning duty (a valid index when there is none)
+        auto win = [&](int j, int bu) { return min(max(blo1 + j - mlo + 1 - sh * max(bu, 0), 0), M + 2); };
+        auto emit = [&](int j, double bc, int bu, double2 src, int rs) {
             double2 out = make_double2(BIG, 0.0);
             int p = 0xFFFF;
-            if (bu >= 0) {                 // the winner's state and source
-                const int mi = min(max(m0 - sh * bu, 0), M + 2);
-                out = make_double2(bc, fma(Ak, L.rmin[mi].y, fma(g, (double)bu, Ck)));
-                p = L.rsrc[mi] | (bu << 12);
+            if (bu >= 0) {
+                out = make_double2(bc, fma(Ak, src.y, fma(g, (double)bu, Ck)));
+                p = rs | (bu << 12);
             }
             lab[j] = out;
             L.par[k * NB_CAP + j] = (uint16_t)p;
             if (more) L.tarr[j] = key(out, blo1 + j, An, r1, c1);
+        };
+        for (int j = jin0 + lane; j <= jin1; j += 2 * nt) {
+            const int j2 = min(j + nt, jin1);              // second target (a repeat past the end)
+            double bc1, bc2;
+            int bu1, bu2;
+            pick(j, bc1, bu1);
+            pick(j2, bc2, bu2);
+            const int i1 = win(j, bu1), i2 = win(j2, bu2);
+            const double2 s1 = L.rmin[i1], s2 = L.rmin[i2];
+            const int r1s = L.rsrc[i1], r2s = L.rsrc[i2];
+            emit(j, bc1, bu1, s1, r1s);
+            if (j + nt <= jin1) emit(j2, bc2, bu2, s2, r2s);
         }
         // boundary buckets: the first cheapest of their per-duty candidates
         for (int q = lane; q < nbnd; q += nt) {
             const int j = q < nleft ? q : jin1 + 1 + (q - nleft);
             Best B{BIG, 0.0, 0xFFFF};
-            for (int u = 0; u <= S; ++u) {
-                const double2 cv = L.cand[q * (S + 1) + u];
-                if (cv.x < B.c) { B.c = cv.x; B.x = cv.y; B.p = L.candp[q * (S + 1) + u]; }
+            if constexpr (SS > 0) {
+                double2 cv[NU];
+                int cp[NU];
+#pragma unroll
+                for (int u = 0; u < NU; ++u) { cv[u] = L.cand[q * NU + u]; cp[u] = L.candp[q * NU + u]; }
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const bool ok = cv[u].x < B.c;
+                    B.c = ok ? cv[u].x : B.c;
+                    B.x = ok ? cv[u].y : B.x;
+                    B.p = ok ? cp[u] : B.p;
+                }
+            } else {
+                for (int u = 0; u <= S; ++u) {
+                    const double2 cv = L.cand[q * (S + 1) + u];
+                    if (cv.x < B.c) { B.c = cv.x; B.x = cv.y; B.p = L.candp[q * (S + 1) + u]; }
+                }
             }
             const double2 out = make_double2(B.c, B.x);
             lab[j] = out;
