@@ -1672,22 +1672,26 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         }
         const double iA = 1.0 / Ak;
         for (int s = lane; s < nbz; s += nt) {
+            // every key and label this bucket may need, read together (the edge reads are
+            // clamped and their values replaced)
             const int T = L.tarr[s];
-            const int Tp = s > 0 ? L.tarr[s - 1] : mlo - 1;
-            const int Tn = s + 1 < nbz ? L.tarr[s + 1] : mhi + 1;
+            int Tp = L.tarr[max(s - 1, 0)], Tn = L.tarr[min(s + 1, nbz - 1)], Tn2 = L.tarr[min(s + 2, nbz - 1)];
             const double2 l0 = lab[s];
             const double2 l1 = lab[min(s + 1, nbz - 1)];
-            for (int m = Tp + 1; m < T; ++m) { L.rmin[m - mlo + 1] = make_double2(BIG, 0.0); L.rsrc[m - mlo + 1] = -1; }
-            if (T > Tp) {
-                double2 bl = l0;
-                int bs = s;
-                if (Tn == T) {
-                    if (l1.x < bl.x) { bl = l1; bs = s + 1; }
+            Tp = s > 0 ? Tp : mlo - 1;
+            Tn = s + 1 < nbz ? Tn : mhi + 1;
+            Tn2 = s + 2 < nbz ? Tn2 : mhi + 1;
+            if (T > Tp + 1)                                   // keys skipped by the map (rare)
+                for (int m = Tp + 1; m < T; ++m) { L.rmin[m - mlo + 1] = make_double2(BIG, 0.0); L.rsrc[m - mlo + 1] = -1; }
+            if (T > Tp) {                                     // s heads the run of key T
+                const bool take1 = Tn == T && l1.x < l0.x;
+                double2 bl = take1 ? l1 : l0;
+                int bs = take1 ? s + 1 : s;
+                if (Tn2 == T)                                 // runs of 3+ (A_k < 2/3)
                     for (int s2 = s + 2; s2 < nbz && L.tarr[s2] == T; ++s2) {
                         const double2 lv = lab[s2];
                         if (lv.x < bl.x) { bl = lv; bs = s2; }
                     }
-                }
                 L.rmin[T - mlo + 1] = bl;
                 L.rsrc[T - mlo + 1] = (int16_t)bs;
             }
@@ -1696,7 +1700,9 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         // located from the near-linear key map (T_s ~ A s) and walked to, then every member is
         // tested against the exact box
         for (int idx = lane; idx < nbnd * (S + 1); idx += nt) {
-            const int q = idx / (S + 1), u = idx - q * (S + 1);
+            constexpr int NUC = SS > 0 ? SS + 1 : 1;           // compile-time divisor when known
+            const int q = SS > 0 ? idx / NUC : idx / (S + 1);
+            const int u = idx - q * (S + 1);
             const int j = q < nleft ? q : jin1 + 1 + (q - nleft);
             const int m = blo1 + j - sh * u;
             Best B{BIG, 0.0, 0xFFFF};
