@@ -85,27 +85,11 @@ class DeviceAggregator:
                           "(the reference raises here, mpc_calc.py:280-289 / 537-539)")
 
     def collected_data(self):
-        """This shard's `collected_data` dict (aggregator.py:589-615, 737-748 append order)."""
-        keys = ["p_grid_opt", "forecast_p_grid_opt", "p_load_opt", "temp_in_opt", "temp_wh_opt",
-                "hvac_cool_on_opt", "hvac_heat_on_opt", "wh_heat_on_opt", "cost_opt", "waterdraws",
-                "correct_solve"]
+        """This shard's `collected_data` dict (aggregator.py:589-615, 737-748): the initial
+        entries plus every step's hash fields, in the reference's key order."""
+        from . import results as R
         hist = self.hist[:self.timestep].cpu().numpy()
-        out = {}
-        for i, h in enumerate(self.homes):
-            d = {"type": h["type"], "temp_in_sp": h["hvac"]["temp_in_sp"], "temp_wh_sp": h["wh"]["temp_wh_sp"],
-                 "temp_in_opt": [h["hvac"]["temp_in_init"]], "temp_wh_opt": [h["wh"]["temp_wh_init"]]}
-            ks = list(keys)
-            if "pv" in h["type"]:
-                ks += ["p_pv_opt", "u_pv_curt_opt"]
-            if "battery" in h["type"]:
-                ks += ["p_batt_ch", "p_batt_disch", "e_batt_opt"]
-                d["e_batt_opt"] = [h["battery"]["e_batt_init"]]
-            for k in ks:
-                d.setdefault(k, [])
-                col = hist[:, L.K[k], i]
-                d[k] += [float(v) for v in col if not np.isnan(v)]
-            out[h["name"]] = d
-        return out
+        return R.append_history(R.new_collected(self.homes), self.homes, hist)
 
     def summary(self):
         agg = self.agg_hist[:self.timestep].cpu().numpy()

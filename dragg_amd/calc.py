@@ -1,0 +1,78 @@
+"""Per-home facade with the reference's `MPCCalc` interface (mpc_calc.py:16-98, 649-672).
+
+For code written against `MPCCalc(home).run_home()` + `manage_home` under a pool map
+(aggregator.py:723-724).  `MPCCalc` objects registered on one `Community` share a single
+device batch: the first `run_home()` of a timestep launches the solver for EVERY home of the
+community (one `dragg_mpc_step`), the other homes find their results already in the device
+hash.  Calling `run_home()` for every home of a step, in any order, is therefore the
+reference's `pool.map(manage_home, homes)`; a home whose solve hits one of the reference's
+crashing paths raises the reference's exception from its own `run_home()`.
+
+The home's redis hash is the device hash: `Community.hgetall(name)` returns it with the
+reference's field names and str values, as redis does; `MPCCalc.optimal_vals` holds the
+home's hash after its latest step, as numbers.
+"""
+from . import _lib as L
+from .inputs import max_load
+from .mpc import MPCBatch
+
+
+class Community:
+    """The redis side of a run for a set of homes: environment lists, `current_values`
+    timestep, `reward_price`, and the per-home hashes (device resident)."""
+
+    def __init__(self, homes, oat, ghi, tou, start_hour_index, reward_price=(0.0,), int_mode="round", seed=0,
+                 device="cuda"):
+        self.batch = MPCBatch(homes, oat, ghi, tou, start_hour_index, reward_price, int_mode=int_mode, seed=seed,
+                              device=device)
+        self.index = {h["name"]: i for i, h in enumerate(homes)}
+        self.timestep = 0
+        self._solved = -1
+        self._status = None
+
+    # aggregator.py:664-675 (redis_set_current_values)
+    def set_timestep(self, t):
+        self.timestep = int(t)
+
+    def set_reward_price(self, rp):
+        self.batch.set_reward_price(rp)
+
+    def solve(self):
+        """Solve every home for the current timestep (once per timestep)."""
+        if self._solved != self.timestep:
+            self.batch.step(self.timestep)
+            self._status = self.batch.status.cpu().numpy()
+            self._solved = self.timestep
+        return self._status
+
+    def hgetall(self, name):
+        return self.batch.hash_dict(self.index[name], as_str=True)
+
+
+def manage_home(home):
+    """mpc_calc.py:16-22."""
+    home.run_home()
+
+
+class MPCCalc:
+    def __init__(self, home, community):
+        self.home = home
+        self.name = home["name"]
+        self.type = home["type"]
+        self.community = community
+        self.i = community.index[self.name]
+        self.max_load = max_load(home)
+        self.timestep = 0
+        self.optimal_vals = {}
+
+    def run_home(self):
+        """One timestep of this home (mpc_calc.py:649-672)."""
+        st = int(self.community.solve()[self.i])
+        if st == L.ST_ERR_MISSING:
+            raise KeyError("e_batt_opt" if "battery" in self.type else "temp_in_opt")
+        if st == L.ST_ERR_PARSE:
+            raise ValueError("could not convert string to float: '-'")
+        self.timestep = self.community.timestep
+        self.optimal_vals = self.community.batch.hash_dict(self.i, as_str=False)
+        self.counter = int(self.optimal_vals.get("solve_counter", 0))
+        return None

@@ -15,6 +15,12 @@ def load(name):
         return json.load(f)
 
 
+def config_text(params):
+    """The scenario's config.toml (tests/golden/config_template.toml, as make_golden.py wrote it)."""
+    with open(os.path.join(GOLDEN, "config_template.toml")) as f:
+        return f.read().format(**params)
+
+
 def scenarios():
     return sorted(f[:-8] for f in os.listdir(GOLDEN) if f.endswith(".json.gz"))
 
