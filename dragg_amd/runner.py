@@ -30,7 +30,7 @@ from . import results as R
 
 class Aggregator:
     def __init__(self, data_dir=None, config_file=None, outputs_dir="outputs", int_mode="round", device=None,
-                 group=None, first_name=None):
+                 group=None, first_name=None, batch_cls=None):
         env = os.environ
         self.data_dir = os.path.expanduser(env.get("DATA_DIR", "data")) if data_dir is None else data_dir
         self.outputs_dir = outputs_dir
@@ -52,6 +52,7 @@ class Aggregator:
         self.case = "baseline"
         self.int_mode, self.device, self.group = int_mode, device, group
         self.first_name = first_name
+        self.batch_cls = batch_cls          # injectable only for the CPU tests of the multi-rank glue
         self.rank, self.world = 0, 1
         try:
             import torch.distributed as dist
@@ -97,7 +98,8 @@ class Aggregator:
         self.dev = DeviceAggregator(self.checked, col("OAT"), col("GHI"), col("tou"), self.start_hour_index,
                                     self.num_timesteps, reward_price=self.reward_price, int_mode=self.int_mode,
                                     seed=int(self.config["simulation"]["random_seed"]), rank=self.rank,
-                                    world=self.world, group=self.group, device=self.device)
+                                    world=self.world, group=self.group, device=self.device,
+                                    **({"batch_cls": self.batch_cls} if self.batch_cls else {}))
         for t in range(self.num_timesteps):
             noise = noise_fn(t)[:, self.dev.lo:self.dev.hi] if noise_fn is not None else None
             self.dev.run_iteration(noise)
@@ -156,7 +158,18 @@ class Aggregator:
 
 
 def main():
-    Aggregator().run()
+    """`python -m dragg_amd.runner`; under torchrun (WORLD_SIZE > 1) one rank per GPU over RCCL."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group("nccl")
+        try:
+            Aggregator().run()
+        finally:
+            dist.destroy_process_group()
+    else:
+        Aggregator().run()
 
 
 if __name__ == "__main__":

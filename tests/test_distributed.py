@@ -88,3 +88,59 @@ def test_shard_bounds_cover():
             parts = [shard_bounds(n, r, w) for r in range(w)]
             assert parts[0][0] == 0 and parts[-1][1] == n
             assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+
+
+# ------------------------------------------------------------------ the runner over 2 ranks
+class HashBatch(FakeBatch):
+    """Stand-in that writes every hash field: value = global home index + 100 t."""
+
+    def step(self, t, noise=None, hist=None):
+        self.t = t
+        if hist is not None:
+            v = torch.arange(self.off, self.off + self.N, dtype=torch.float64) + 100.0 * t
+            hist.copy_(v.expand_as(hist))
+
+
+def _runner_worker(rank, world, port, root, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dragg_amd.runner import Aggregator
+    a = Aggregator(data_dir=os.path.join(root, "data"), outputs_dir=os.path.join(root, "outputs"),
+                   device=torch.device("cpu"), batch_cls=HashBatch)
+    path = a.run()
+    q.put((rank, a.dev.lo, a.dev.hi, path))
+    dist.destroy_process_group()
+
+
+def test_runner_two_ranks_gathers_history(tmp_path):
+    """Two ranks each solve a contiguous shard; rank 0 gathers the hash history and writes
+    results.json with every home's series in community order."""
+    import json
+    from tests import fixtures as F
+    from tests.test_runner import _synthetic_data
+    data = tmp_path / "data"
+    data.mkdir()
+    _synthetic_data(str(data))
+    params = dict(n=7, batt=2, pv=2, pvb=1, start="2015-01-01 00", end="2015-01-01 03", dt=4, horizon=2,
+                  action_horizon=2, seed=3)
+    with open(data / "config.toml", "w") as f:
+        f.write(F.config_text(params))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_runner_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[1][3] is None and res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == 7
+    with open(res[0][3]) as f:
+        out = json.load(f)
+    names = [k for k in out if k != "Summary"]
+    assert len(names) == 7
+    T = 12
+    for i, n in enumerate(names):
+        assert out[n]["p_grid_opt"] == [i + 100.0 * t for t in range(T)]
+    assert out["Summary"]["p_grid_aggregate"] == [sum(i + 100.0 * t for i in range(7)) for t in range(T)]
