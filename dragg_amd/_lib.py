@@ -8,7 +8,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdragg_mi355x.so")
+# DRAGG_LIB: an alternative build of the same library (kernel experiments); default in-tree
+LIB_PATH = os.environ.get("DRAGG_LIB") or os.path.join(HERE, "libdragg_mi355x.so")
 
 ABI_VERSION = 3
 
