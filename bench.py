@@ -44,6 +44,11 @@ def parse():
     ap.add_argument("--int-mode", default="round", choices=["round", "relax", "round_lp"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--cpu-workers", type=int, default=0)
+    ap.add_argument("--workload", default="rbo", choices=["rbo", "rl"],
+                    help="rbo: run_rbo_mpc closed loop (configs[2], default); rl: configs[4], every step "
+                         "is one RL reward-price action: price broadcast, --forecast-horizon rollout "
+                         "re-solves of the community, the committed step, the sums to the host")
+    ap.add_argument("--forecast-horizon", type=int, default=1, help="rl: rollout timesteps per action")
     return ap.parse_args()
 
 
@@ -163,17 +168,34 @@ def main():
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    rl = args.workload == "rl"
+    fh = args.forecast_horizon if rl else 0
+    import numpy as np
+    prices = np.random.default_rng(5).uniform(-0.02, 0.02, (total_steps, 1)) * np.ones((1, Hh * dt))
+
+    def action(k):
+        """rl: one reward-price action (random stand-in for the host agent's choice)."""
+        agg.set_reward_price(prices[k])
+        agg.forecast(fh)
+
+    for k in range(args.warmup):
+        if rl:
+            action(k)
         agg.run_iteration()
         agg.collect_data()
     barrier()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
+        if rl:
+            action(args.warmup + k)
         evs[k][0].record(stream)
         agg.run_iteration()
         evs[k][1].record(stream)
-        agg.collect_data()
+        if rl:
+            agg.collect_data().tolist()         # the agent reads the community sums on the host
+        else:
+            agg.collect_data()
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -185,12 +207,16 @@ def main():
     success = float((st == 0).float().mean())
     stat_counts = {name: int((st == i).sum()) for i, name in enumerate(
         ["optimal", "infeasible", "infeasible_cert", "max_iter", "round_fail", "err_parse", "err_missing"])}
-    solves = n_total * args.steps
+    solves = n_total * args.steps * (1 + fh)
     value = solves / elapsed
     if rank == 0:
         H = agg.batch.H
         workload = (f"{n_total} homes x {args.steps} closed-loop {60 // dt}-min steps, H={H} "
                     f"({Hh} h), month {args.month}, run_rbo_mpc, int_mode={args.int_mode}")
+        if rl:
+            workload = (f"{n_total} homes x {args.steps} RL reward-price actions, each {fh} rollout "
+                        f"timestep(s) + the committed {60 // dt}-min step, H={H} ({Hh} h), month {args.month}, "
+                        f"run_rl_agg, int_mode={args.int_mode}")
         achieved = bytes_per_launch(agg.batch, success) / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src = measured_traffic(traffic_key(n_total, H, dt, args.month, args.int_mode, world))
         out = {
@@ -199,7 +225,7 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (NSRDB-shaped weather, config.toml-range homes, seeded)",
-            "config": {"workload": workload, "baseline_config": "BASELINE.json configs[2]",
+            "config": {"workload": workload, "baseline_config": "BASELINE.json configs[4]" if rl else "BASELINE.json configs[2]",
                        "homes_total": n_total, "homes_per_gpu": agg.batch.N, "global_batch": n_total,
                        "horizon": H, "mix": "40/20/20/20 base/pv/battery/pv_battery",
                        "parallelism": f"homes sharded x{world}"},

@@ -36,6 +36,7 @@ class DeviceAggregator:
         self.all_homes = homes
         self.homes = homes[lo:hi]
         dev = device or torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
         # batch_cls is injectable only so the multi-rank glue can be exercised with gloo on
         # CPU (tests/test_distributed.py); the solver itself is MPCBatch (HIP, no fallback).
         self.batch = batch_cls(self.homes, oat, ghi, tou, start_index, reward_price, int_mode=int_mode,
@@ -73,6 +74,48 @@ class DeviceAggregator:
             self.run_iteration(noise_fn(self.timestep) if noise_fn else None)
             self.collect_data()
         return self.agg_hist[:self.timestep]
+
+    # ------------------------------------------------------------------ RL reward-price path
+    # (aggregator.py:664-675, 876-896).  A step reads exactly three things
+    # that change between steps: the timestep, the hash arrays (vals, fc: the previous
+    # solve, mpc_calc.py:264-289, 527-595) and the reward-price list.  A forecast rollout
+    # therefore snapshots the hash arrays on device, solves ahead and puts them back.
+    def set_reward_price(self, rp, src=0):
+        """Broadcast the reward-price list decided on rank `src` (the RL agent's host) to every
+        rank (one RCCL broadcast of action_horizon*dt fp64) and hand it to the solver."""
+        t = torch.as_tensor(np.asarray(rp, dtype=float) if not torch.is_tensor(rp) else rp,
+                            dtype=torch.float64).to(self.device).reshape(-1).contiguous()
+        if self.world > 1:
+            torch.distributed.broadcast(t, src=src, group=self.group)
+        self.batch.set_reward_price(t)
+        return t
+
+    def snapshot(self):
+        return self.timestep, self.batch.vals.clone(), self.batch.fc.clone()
+
+    def restore(self, snap):
+        t, vals, fc = snap
+        self.timestep = t
+        self.batch.vals.copy_(vals)
+        self.batch.fc.copy_(fc)
+
+    def forecast(self, steps, noise_fn=None):
+        """Solve every home `steps` timesteps ahead under the current reward price without
+        committing anything (no history, state restored): the community's [steps][agg_load,
+        forecast_load, agg_cost], all-reduced once over the ranks.  The season-noise stream
+        is keyed by (seed, home, t), so a rollout sees the draws the committed steps will."""
+        snap = self.snapshot()
+        out = torch.empty((steps, 3), dtype=torch.float64, device=self.device)
+        try:
+            for s in range(steps):
+                t = self.timestep + s
+                self.batch.step(t, noise=noise_fn(t) if noise_fn else None, hist=None)
+                out[s].copy_(self.batch.aggregate())
+        finally:
+            self.restore(snap)
+        if self.world > 1:
+            torch.distributed.all_reduce(out, group=self.group)
+        return out
 
     def check_errors(self):
         """Raise as the reference would if a home hit a crashing path (KeyError / ValueError)."""

@@ -150,13 +150,20 @@ class MPCBatch:
         self.dims.n_env = int(min(len(oat), len(ghi), len(tou)))
 
     def set_reward_price(self, rp):
-        rp = np.asarray([float(v) for v in rp], dtype=float)
-        if len(rp) != 1 and len(rp) < self.H:
+        """The redis 'reward_price' list (mpc_calc.py:630-637): host values, or a device tensor
+        (e.g. an RL action broadcast over RCCL), taken without a host round trip."""
+        if torch.is_tensor(rp):
+            rp = rp.detach().to(device=self.device, dtype=torch.float64).reshape(-1).contiguous()
+            n = rp.numel()
+        else:
+            rp = np.asarray([float(v) for v in rp], dtype=float)
+            n = len(rp)
+        if n != 1 and n < self.H:
             # np.array(rp[:H]) + tou[:H] raises in the reference (mpc_calc.py:353)
-            raise ValueError(f"operands could not be broadcast together: reward_price has {len(rp)} "
+            raise ValueError(f"operands could not be broadcast together: reward_price has {n} "
                              f"entries, horizon is {self.H}")
-        self.rp = torch.tensor(rp, dtype=torch.float64, device=self.device)
-        self.dims.n_rp = len(rp)
+        self.rp = rp if torch.is_tensor(rp) else torch.tensor(rp, dtype=torch.float64, device=self.device)
+        self.dims.n_rp = n
 
     # ------------------------------------------------------------------ structs
     def _problem(self):

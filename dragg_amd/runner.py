@@ -15,8 +15,11 @@ Multi-GPU: start one process per GPU (torchrun) with torch.distributed initialis
 (backend "nccl" = RCCL); homes are sharded in contiguous blocks, the three per-step sums are
 all-reduced, rank 0 gathers the history and writes the files.
 
-Scope: run_rbo_mpc (the baseline case).  SPP prices (`agg.spp_enabled`, an ERCOT xlsx) and
-the RL-aggregator case are not part of this build and raise.
+Scope: run_rbo_mpc (the baseline case) and the RL-aggregator hooks (SURVEY.md §8 F4:
+`setup_rl_agg_run`, `redis_set_current_values`, `gen_setpoint`, `test_response`, plus
+`rl_step` / `rl_forecast` / `run_rl_agg`, the reward-price loop the reference leaves to an
+external driver).  SPP prices (`agg.spp_enabled`, an ERCOT xlsx absent from the reference)
+raise.
 """
 import json
 import os
@@ -60,6 +63,8 @@ class Aggregator:
                 self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         except ImportError:
             pass
+        self.agg_load = 0                   # aggregator.py:55-57
+        self.baseline_agg_load_list = []
         self.max_agg_load_list = []
         self.dev = None
         if self.rank == 0:
@@ -87,12 +92,9 @@ class Aggregator:
             R.write_home_configs(self.outputs_dir, self.all_homes, n)
         self.max_poss_load = sum(I.max_load(h) for h in self.all_homes)
 
-    # aggregator.py:757-778
-    def run_baseline(self, noise_fn=None):
-        """`noise_fn(t)`, optional: the season draw [H][homes checked] of step t (replaces the
-        keyed on-device stream, e.g. to replay a recorded run)."""
+    def _device_community(self):
+        """The checked homes (aggregator.py:762-765 / 879-882) as this rank's device shard."""
         from .aggregator import DeviceAggregator
-        self.start_time = datetime.now()
         self.checked = [h for h in self.all_homes if self.check_type == "all" or h["type"] == self.check_type]
         col = lambda c: self.all_data[c].to_numpy(dtype=float)  # noqa: E731
         self.dev = DeviceAggregator(self.checked, col("OAT"), col("GHI"), col("tou"), self.start_hour_index,
@@ -100,6 +102,14 @@ class Aggregator:
                                     seed=int(self.config["simulation"]["random_seed"]), rank=self.rank,
                                     world=self.world, group=self.group, device=self.device,
                                     **({"batch_cls": self.batch_cls} if self.batch_cls else {}))
+        return self.dev
+
+    # aggregator.py:757-778
+    def run_baseline(self, noise_fn=None):
+        """`noise_fn(t)`, optional: the season draw [H][homes checked] of step t (replaces the
+        keyed on-device stream, e.g. to replay a recorded run)."""
+        self.start_time = datetime.now()
+        self._device_community()
         for t in range(self.num_timesteps):
             noise = noise_fn(t)[:, self.dev.lo:self.dev.hi] if noise_fn is not None else None
             self.dev.run_iteration(noise)
@@ -108,6 +118,119 @@ class Aggregator:
             if (t + 1) % self.checkpoint_interval == 0:
                 self.write_outputs()
         self.dev.check_errors()
+
+    # ------------------------------------------------------------------ RL aggregator (§8 F4)
+    # aggregator.py:677-696
+    def gen_setpoint(self):
+        if self.timestep < 2:
+            self.tracked_loads = [0.5 * self.max_poss_load] * self.config["agg"]["rl"]["prev_timesteps"]
+            self.max_load = -float("inf")
+            self.min_load = float("inf")
+        else:
+            self.tracked_loads[:-1] = self.tracked_loads[1:]
+            self.tracked_loads[-1] = self.agg_load
+        self.avg_load = np.average(self.tracked_loads)
+        if self.agg_load > self.max_load or self.timestep % 24 == 0:
+            self.max_load = self.agg_load
+        if self.agg_load < self.min_load or self.timestep % 24 == 0:
+            self.min_load = self.agg_load
+        return self.avg_load
+
+    # aggregator.py:664-675: the reward price goes to every rank's solver (RCCL broadcast from
+    # rank 0) instead of the redis 'reward_price' list
+    def redis_set_current_values(self):
+        if "rl" in self.case:
+            self.all_sps[self.timestep] = self.agg_setpoint
+            self.all_rps[self.timestep] = self.reward_price[0]
+            self.dev.set_reward_price(self.reward_price)
+
+    # aggregator.py:876-896
+    def setup_rl_agg_run(self, noise_fn=None):
+        """Needs the community (`get_homes`) like the reference's (it reads all_homes_obj)."""
+        self.flush()
+        self._device_community()
+        self.noise_fn = noise_fn
+        self.start_time = datetime.now()
+        self.baseline_agg_load_list = [0]
+        self.all_rewards = []
+        self.forecast_load = 3 * len(self.all_homes)
+        self.prev_forecast_load = self.forecast_load
+        self.forecast_setpoint = self.gen_setpoint()
+        self.agg_load = self.forecast_load  # approximate load for initial timestep
+        self.agg_setpoint = self.gen_setpoint()
+        self.redis_set_current_values()
+
+    def _noise(self, t):
+        fn = getattr(self, "noise_fn", None)
+        return fn(t)[:, self.dev.lo:self.dev.hi] if fn is not None else None
+
+    # aggregator.py:728-755 on the RL path: the three community sums come to the host (the
+    # agent needs them) and feed the setpoint
+    def collect_data(self):
+        agg = self.dev.collect_data().tolist()
+        self.agg_load, self.forecast_load, self.agg_cost = agg
+        self.baseline_agg_load_list.append(self.agg_load)
+        self.agg_setpoint = self.gen_setpoint()
+        return agg
+
+    def _set_price(self, reward_price):
+        rp = np.asarray(reward_price, dtype=float).reshape(-1)
+        if len(rp) == 1:
+            rp = np.full(len(self.reward_price), rp[0])
+        if len(rp) != len(self.reward_price):
+            raise ValueError(f"reward price has {len(rp)} entries, the action horizon holds "
+                             f"{len(self.reward_price)} (agg.rl.action_horizon * dt)")
+        self.reward_price = rp
+
+    def rl_step(self, reward_price):
+        """One RL-aggregator timestep under `reward_price` (a scalar, or action_horizon*dt
+        values): publish the price, solve every home, collect, new setpoint -- the order of
+        the reference's step loop (aggregator.py:768-771)."""
+        self._set_price(reward_price)
+        self.redis_set_current_values()
+        self.dev.run_iteration(self._noise(self.dev.timestep))
+        self.timestep = self.dev.timestep
+        return self.collect_data()
+
+    def rl_forecast(self, reward_price, steps=None):
+        """The community's response to a candidate price over `rl.forecast_horizon` timesteps
+        (README.md:67, `rl_agg_forecast_horizon`): every home re-solved ahead on device,
+        nothing committed.  -> [steps][agg_load, forecast_load, agg_cost] on the host."""
+        steps = int(self.config["agg"]["rl"]["forecast_horizon"]) if steps is None else int(steps)
+        steps = min(steps, self.num_timesteps - self.dev.timestep)
+        prev = self.reward_price
+        self._set_price(reward_price)
+        self.dev.set_reward_price(self.reward_price)
+        try:
+            out = self.dev.forecast(steps, noise_fn=self._noise if getattr(self, "noise_fn", None) else None)
+        finally:
+            self.reward_price = prev
+            self.dev.set_reward_price(prev)
+        return out.cpu().numpy()
+
+    # aggregator.py:898-911
+    def test_response(self):
+        c = self.config["agg"]["simplified"]["response_rate"]
+        if self.timestep == 0:
+            self.agg_load = self.agg_setpoint + 0.1 * self.agg_setpoint
+        self.agg_load = self.agg_load - c * self.reward_price[0] * (self.agg_setpoint - self.agg_load)
+        self.agg_cost = self.agg_load * self.reward_price[0]
+        self.timestep += 1
+
+    def run_rl_agg(self, policy, noise_fn=None):
+        """The `run_rl_agg` case (README.md:55): MPC homes under an RL-designed reward price.
+        `policy(aggregator) -> reward price` is called once per timestep (e.g. an
+        `dragg_amd.rl.RLAgent`'s `act`); it may call `rl_forecast` to try candidate prices.
+        Writes `<run dir>/rl_agg/results.json` with the Summary's RP and p_grid_setpoint."""
+        self.case = "rl_agg"
+        self.get_homes()
+        self.setup_rl_agg_run(noise_fn)
+        for t in range(self.num_timesteps):
+            self.rl_step(policy(self))
+            if (t + 1) % self.checkpoint_interval == 0:
+                self.write_outputs()
+        self.dev.check_errors()
+        return self.write_outputs()
 
     def _history(self):
         """The checked homes' hash history [T][19][N] on rank 0 (gathered from every rank)."""
@@ -127,7 +250,8 @@ class Aggregator:
         t_diff = datetime.now() - self.start_time
         collected = R.new_collected(self.all_homes)
         R.append_history(collected, self.checked, hist)
-        loads = R.aggregate_loads(hist)
+        # the RL case's list starts with setup_rl_agg_run's 0 (aggregator.py:887)
+        loads = self.baseline_agg_load_list if "rl" in self.case else R.aggregate_loads(hist)
         self.max_agg_load = max(loads)
         self.max_agg_load_list.append(self.max_agg_load)
         collected["Summary"] = R.summary(
@@ -154,7 +278,10 @@ class Aggregator:
             self.get_homes()
             self.run_baseline(noise_fn)
             return self.write_outputs()
-        raise NotImplementedError("only run_rbo_mpc (the baseline case) is part of this build")
+        if sim.get("run_rl_agg"):
+            from .rl import agent_policy
+            return self.run_rl_agg(agent_policy(self), noise_fn)
+        return None
 
 
 def main():
