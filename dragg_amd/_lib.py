@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # DRAGG_LIB: an alternative build of the same library (kernel experiments); default in-tree
 LIB_PATH = os.environ.get("DRAGG_LIB") or os.path.join(HERE, "libdragg_mi355x.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # enums (mirror include/dragg_mi355x.h)
 BASE, PV_ONLY, BATTERY_ONLY, PV_BATTERY = 0, 1, 2, 3
@@ -53,7 +53,8 @@ class Dims(ctypes.Structure):
 class Problem(ctypes.Structure):
     _fields_ = [("params", c_dp), ("home_type", c_dp), ("draw_hourly", c_dp), ("oat", c_dp), ("ghi", c_dp),
                 ("tou", c_dp), ("reward_price", c_dp), ("start_index", ctypes.c_int32),
-                ("home_offset", ctypes.c_int32), ("seed", ctypes.c_uint64), ("workspace", c_dp)]
+                ("home_offset", ctypes.c_int32), ("seed", ctypes.c_uint64), ("workspace", c_dp),
+                ("home_stride", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class Hash(ctypes.Structure):
@@ -103,7 +104,7 @@ def load(path=LIB_PATH):
                                              ctypes.POINTER(Out), c_dp]
     lib.dragg_mpc_aggregate.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Hash), c_dp, c_dp]
     lib.dragg_mpc_season_noise.argtypes = [ctypes.POINTER(Dims), ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
-                                           c_dp, c_dp]
+                                           ctypes.c_int32, c_dp, c_dp]
     if lib.dragg_mpc_abi_version() != ABI_VERSION:
         raise DraggError("ABI version mismatch between dragg_amd and libdragg_mi355x.so")
     _LIB = lib

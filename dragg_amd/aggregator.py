@@ -22,8 +22,12 @@ from . import _lib as L
 from .mpc import MPCBatch
 
 
-def shard_bounds(n, rank, world):
-    return (n * rank) // world, (n * (rank + 1)) // world
+def shard_index(n, rank, world):
+    """Global indices of the homes a rank solves: every world-th home from `rank`.  Strided
+    rather than contiguous so that every shard carries the community's type mix (the
+    reference lists homes grouped by type, aggregator.py:425-587, and battery homes cost more
+    per solve): the ranks finish a step together."""
+    return np.arange(rank, n, world)
 
 
 class DeviceAggregator:
@@ -31,16 +35,15 @@ class DeviceAggregator:
                  int_mode="round", seed=0, rank=0, world=1, group=None, keep_history=True,
                  max_iter=4000, check_every=10, device=None, batch_cls=MPCBatch):
         self.rank, self.world, self.group = rank, world, group
-        lo, hi = shard_bounds(len(homes), rank, world)
-        self.lo, self.hi = lo, hi
+        self.index = shard_index(len(homes), rank, world)
         self.all_homes = homes
-        self.homes = homes[lo:hi]
+        self.homes = [homes[i] for i in self.index]
         dev = device or torch.device("cuda", torch.cuda.current_device())
         self.device = dev
         # batch_cls is injectable only so the multi-rank glue can be exercised with gloo on
         # CPU (tests/test_distributed.py); the solver itself is MPCBatch (HIP, no fallback).
         self.batch = batch_cls(self.homes, oat, ghi, tou, start_index, reward_price, int_mode=int_mode,
-                              seed=seed, home_offset=lo, max_iter=max_iter, check_every=check_every,
+                              seed=seed, home_offset=rank, home_stride=world, max_iter=max_iter, check_every=check_every,
                               device=dev)
         self.num_timesteps = num_timesteps
         self.timestep = 0

@@ -106,6 +106,50 @@ DEV double wave_sum(double v) {
 }
 DEV bool wave_any(bool p) { return __any(p); }
 
+// Wave-wide reductions and scans on DPP lane moves (VALU, no LDS round trip as __shfl_*'s
+// ds_bpermute takes): butterfly inside each 16-lane row (quad_perm xor 1, xor 2, half-row
+// and row mirrors), then the four row results read into scalars and combined in row order.
+// Every lane returns the same value; the combination order is fixed, so results are
+// deterministic.
+template <int CTRL, typename T>
+DEV T dpp_mov(T v) { return __builtin_amdgcn_update_dpp((T)0, v, CTRL, 0xf, 0xf, true); }
+// v_readlane on the 32-bit halves (the builtin takes an int: a double would be converted)
+DEV int read_lane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+DEV double read_lane(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <typename T, typename Op>
+DEV T dpp_reduce(T v, Op op) {
+    v = op(v, dpp_mov<0xB1>(v));          // quad_perm [1,0,3,2]
+    v = op(v, dpp_mov<0x4E>(v));          // quad_perm [2,3,0,1]
+    v = op(v, dpp_mov<0x141>(v));         // row_half_mirror
+    v = op(v, dpp_mov<0x140>(v));         // row_mirror
+    const T r0 = read_lane(v, 0), r1 = read_lane(v, 16);
+    const T r2 = read_lane(v, 32), r3 = read_lane(v, 48);
+    return op(op(r0, r1), op(r2, r3));
+}
+DEV double dpp_sum(double v) { return dpp_reduce(v, [](double a, double b) { return a + b; }); }
+DEV int dpp_isum(int v) { return dpp_reduce(v, [](int a, int b) { return a + b; }); }
+DEV int dpp_imin(int v) { return dpp_reduce(v, [](int a, int b) { return min(a, b); }); }
+DEV int dpp_imax(int v) { return dpp_reduce(v, [](int a, int b) { return max(a, b); }); }
+// inclusive prefix sum over the 64 lanes: Hillis-Steele inside each row (row_shr 1, 2, 4, 8;
+// lanes shifted in from outside the row read 0), then the totals of the rows below added
+DEV double dpp_scan(double v, int lane) {
+    v += dpp_mov<0x111>(v);
+    v += dpp_mov<0x112>(v);
+    v += dpp_mov<0x114>(v);
+    v += dpp_mov<0x118>(v);
+    const double t0 = read_lane(v, 15), t1 = read_lane(v, 31);
+    const double t2 = read_lane(v, 47);
+    const int row = lane >> 4;
+    const double t01 = t0 + t1;
+    const double off = row == 0 ? 0.0 : row == 1 ? t0 : row == 2 ? t01 : t01 + t2;
+    return row == 0 ? v : v + off;
+}
+
 // order LDS accesses between the lanes of ONE wave (code running on a single wave of a
 // multi-wave workgroup must not use __syncthreads)
 DEV void wave_sync() {
@@ -1193,7 +1237,7 @@ DEV int prologue(const KArgs& a, Home& h, const Lds& L, const Io& io, int lane, 
             if (a.noise) z = a.noise[(size_t)k * N + home];
             else {
                 double z0, z1;
-                normal_pair(a.p.seed, a.p.home_offset + home, t, k >> 1, &z0, &z1);
+                normal_pair(a.p.seed, a.p.home_offset + home * max(a.p.home_stride, 1), t, k >> 1, &z0, &z1);
                 z = (k & 1) ? z1 : z0;
             }
             mx = fmax(mx, a.p.oat[s0 + k + 1] + pow(1.1, (double)k) * z);
@@ -1756,13 +1800,23 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
 #pragma unroll
                     for (int u = 0; u < NU; ++u) lv[u] = L.rmin[min(max(m0 - sh * u, 0), M + 2)].x;
                 }
+                // first cheapest duty by a pairwise tournament (the right operand wins only when
+                // strictly cheaper, so ties keep the lower duty): log2 depth instead of a chain
+                double cv[NU];
+                int cu[NU];
 #pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    const double cn = fma(ck, (double)u, lv[u]);
-                    const bool ok = cn < bc;
-                    bc = ok ? cn : bc;
-                    bu = ok ? u : bu;
-                }
+                for (int u = 0; u < NU; ++u) { cv[u] = fma(ck, (double)u, lv[u]); cu[u] = u; }
+#pragma unroll
+                for (int st = 1; st < NU; st <<= 1)
+#pragma unroll
+                    for (int u = 0; u + st < NU; u += 2 * st) {
+                        const bool ok = cv[u + st] < cv[u];
+                        cv[u] = ok ? cv[u + st] : cv[u];
+                        cu[u] = ok ? cu[u + st] : cu[u];
+                    }
+                const bool any = cv[0] < bc;
+                bc = any ? cv[0] : bc;
+                bu = any ? cu[0] : bu;
             } else {
                 for (int u = 0; u <= S; ++u) {
                     const double cn = fma(ck, (double)u, L.rmin[min(max(m0 - sh * u, 0), M + 2)].x);
@@ -1916,10 +1970,8 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
             if (si <= s1) { ++c1; p1 += li; }
             if (si <= s2) { ++c2; p2 += li; }
         }
-        for (int o = 32; o > 0; o >>= 1) {
-            c1 += __shfl_xor(c1, o); c2 += __shfl_xor(c2, o);
-            p1 += __shfl_xor(p1, o); p2 += __shfl_xor(p2, o);
-        }
+        c1 = dpp_isum(c1); c2 = dpp_isum(c2);
+        p1 = dpp_sum(p1); p2 = dpp_sum(p2);
         const int r1 = c1, r2 = c2 + 1;               // merged positions of psi's segments
         p2 += l1;                                     // psi 1 precedes psi 2 (s1 <= s2)
         for (int i = lane; i < n; i += WAVE) {
@@ -1934,7 +1986,7 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
         wave_sync();
         double tot = 0.0;
         for (int i = lane; i < n; i += WAVE) tot += L1[i];
-        tot = wave_sum(tot);
+        tot = dpp_sum(tot);
         if (k == 0) {                                 // E_0 is fixed: it must lie in the domain
             const double p = h.E0 - X0M;
             feasible = p >= -TOL_P * (1 + fabs(h.E0)) && p <= tot + TOL_P * (1 + fabs(h.E0));
@@ -1948,11 +2000,7 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
         const int i0 = lane * per, i1 = min(n, i0 + per);
         double loc = 0.0;
         for (int i = i0; i < i1; ++i) loc += L1[i];
-        double inc = loc;
-        for (int o = 1; o < WAVE; o <<= 1) {
-            const double v = __shfl_up(inc, o);
-            if (lane >= o) inc += v;
-        }
+        const double inc = dpp_scan(loc, lane);
         double pre = inc - loc;
         int first = n, last = -1;
         for (int i = i0; i < i1; ++i) {
@@ -1962,10 +2010,8 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
             L1[i] = fmax(0.0, ne - ns);
             pre = en;
         }
-        for (int o = 32; o > 0; o >>= 1) {
-            first = min(first, __shfl_xor(first, o));
-            last = max(last, __shfl_xor(last, o));
-        }
+        first = dpp_imin(first);
+        last = dpp_imax(last);
         wave_sync();
         const int nn = last >= first ? last - first + 1 : 0;
         for (int i = lane; i < nn; i += WAVE) { S0[i] = S1[first + i]; L0[i] = L1[first + i]; }
@@ -2117,13 +2163,13 @@ __global__ __launch_bounds__(256) void aggregate_kernel(const double* vals, int 
     if (threadIdx.x < 3) out3[threadIdx.x] = red[threadIdx.x][0];
 }
 
-__global__ void noise_kernel(int N, int H, uint64_t seed, int off, int t, double* out) {
+__global__ void noise_kernel(int N, int H, uint64_t seed, int off, int stride, int t, double* out) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const int pairs = (H + 1) / 2;
     if (idx >= N * pairs) return;
     const int home = idx % N, pr = idx / N;
     double z0, z1;
-    normal_pair(seed, off + home, t, pr, &z0, &z1);
+    normal_pair(seed, off + home * stride, t, pr, &z0, &z1);
     out[(size_t)(2 * pr) * N + home] = z0;
     if (2 * pr + 1 < H) out[(size_t)(2 * pr + 1) * N + home] = z1;
 }
@@ -2251,13 +2297,13 @@ int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, 
     return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
 }
 
-int dragg_mpc_season_noise(const dragg_mpc_dims* dims, uint64_t seed, int32_t home_offset, int32_t timestep,
-                           double* noise_out, void* stream) {
+int dragg_mpc_season_noise(const dragg_mpc_dims* dims, uint64_t seed, int32_t home_offset, int32_t home_stride,
+                           int32_t timestep, double* noise_out, void* stream) {
     if (!dims || !noise_out || dims->n_homes < 0 || dims->horizon < 1) return DRAGG_E_ARG;
     const int total = dims->n_homes * ((dims->horizon + 1) / 2);
     if (total == 0) return DRAGG_OK;
     hipLaunchKernelGGL(noise_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                       dims->n_homes, dims->horizon, seed, home_offset, timestep, noise_out);
+                       dims->n_homes, dims->horizon, seed, home_offset, max(home_stride, 1), timestep, noise_out);
     return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
 }
 

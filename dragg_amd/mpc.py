@@ -95,10 +95,13 @@ class MPCBatch:
         battery LP by an exact piecewise-linear DP), 'relax' (the LP relaxation by ADMM + exact
         vertex polish) or 'round_lp' (the relaxation for status / battery, then the integer DP).
     seed : key of the on-device season-noise stream used when no noise is supplied.
+    home_offset, home_stride : global community index of home i is home_offset + i*home_stride
+        (the season-noise key), so a shard draws the same numbers as the whole community.
     """
 
     def __init__(self, homes, oat=None, ghi=None, tou=None, start_index=0, reward_price=(0.0,),
-                 int_mode="round", seed=0, max_iter=4000, check_every=10, device="cuda", home_offset=0):
+                 int_mode="round", seed=0, max_iter=4000, check_every=10, device="cuda", home_offset=0,
+                 home_stride=1):
         if int_mode not in L.INT_MODES:
             raise ValueError(f"int_mode must be one of {sorted(L.INT_MODES)}, not {int_mode!r}")
         self.lib = L.load()
@@ -120,6 +123,7 @@ class MPCBatch:
                            max_iter=max_iter, check_every=check_every, discount=dm["discount"])
         self.seed = int(seed)
         self.home_offset = int(home_offset)
+        self.home_stride = int(home_stride)
         self.set_environment(oat if oat is not None else [0.0], ghi if ghi is not None else [0.0],
                              tou if tou is not None else [0.0], start_index)
         self.set_reward_price(reward_price)
@@ -170,7 +174,8 @@ class MPCBatch:
         return L.Problem(params=L.ptr(self.params), home_type=L.ptr(self.types), draw_hourly=L.ptr(self.draws),
                          oat=L.ptr(self.oat), ghi=L.ptr(self.ghi), tou=L.ptr(self.tou),
                          reward_price=L.ptr(self.rp), start_index=self.start_index,
-                         home_offset=self.home_offset, seed=self.seed, workspace=L.ptr(self.workspace))
+                         home_offset=self.home_offset, seed=self.seed, workspace=L.ptr(self.workspace),
+                         home_stride=self.home_stride)
 
     def _hash(self):
         return L.Hash(vals=L.ptr(self.vals), fc=L.ptr(self.fc))
@@ -225,7 +230,8 @@ class MPCBatch:
 
     def season_noise(self, t, stream=None):
         out = torch.empty((self.H, self.N), dtype=torch.float64, device=self.device)
-        L.check(self.lib.dragg_mpc_season_noise(ctypes.byref(self.dims), self.seed, self.home_offset, int(t), L.ptr(out),
+        L.check(self.lib.dragg_mpc_season_noise(ctypes.byref(self.dims), self.seed, self.home_offset,
+                                                self.home_stride, int(t), L.ptr(out),
                                                 L.stream_ptr(stream)))
         return out
 

@@ -12,7 +12,7 @@ brought to the host only when an output file is written.
     python -m dragg_amd.runner            # like `python -m dragg.main`, DATA_DIR / CONFIG_FILE honoured
 
 Multi-GPU: start one process per GPU (torchrun) with torch.distributed initialised
-(backend "nccl" = RCCL); homes are sharded in contiguous blocks, the three per-step sums are
+(backend "nccl" = RCCL); homes are sharded by stride (shard_index), the three per-step sums are
 all-reduced, rank 0 gathers the history and writes the files.
 
 Scope: run_rbo_mpc (the baseline case) and the RL-aggregator hooks (SURVEY.md §8 F4:
@@ -111,7 +111,7 @@ class Aggregator:
         self.start_time = datetime.now()
         self._device_community()
         for t in range(self.num_timesteps):
-            noise = noise_fn(t)[:, self.dev.lo:self.dev.hi] if noise_fn is not None else None
+            noise = noise_fn(t)[:, self.dev.index] if noise_fn is not None else None
             self.dev.run_iteration(noise)
             self.dev.collect_data()
             self.timestep = t + 1
@@ -162,7 +162,7 @@ class Aggregator:
 
     def _noise(self, t):
         fn = getattr(self, "noise_fn", None)
-        return fn(t)[:, self.dev.lo:self.dev.hi] if fn is not None else None
+        return fn(t)[:, self.dev.index] if fn is not None else None
 
     # aggregator.py:728-755 on the RL path: the three community sums come to the host (the
     # agent needs them) and feed the setpoint
@@ -240,7 +240,12 @@ class Aggregator:
         import torch.distributed as dist
         parts = [None] * self.world if self.rank == 0 else None
         dist.gather_object(hist, parts, dst=0, group=self.group)
-        return np.concatenate(parts, axis=2) if self.rank == 0 else None
+        if self.rank != 0:
+            return None
+        out = np.empty(hist.shape[:2] + (len(self.checked),), dtype=hist.dtype)
+        for r, p in enumerate(parts):          # rank r holds homes r, r + world, ... (shard_index)
+            out[:, :, r::self.world] = p
+        return out
 
     # aggregator.py:783-844 (summarize_baseline + write_outputs)
     def write_outputs(self):

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DRAGG_MPC_ABI_VERSION 3
+#define DRAGG_MPC_ABI_VERSION 4
 
 /* home types (aggregator.py:425, 468, 520, 555); bit 0 = pv, bit 1 = battery */
 enum dragg_home_type {
@@ -134,6 +134,9 @@ typedef struct dragg_mpc_problem {
     void* workspace;            /* device scratch, dragg_mpc_workspace_bytes(dims) bytes */
                                 /* (int_mode round: DP back-pointers); may be NULL when  */
                                 /* that size is 0                                        */
+    int32_t home_stride;        /* global index of home i = home_offset + i*home_stride */
+                                /* (strided shards; 0 or 1 = a contiguous shard)         */
+    int32_t reserved;
 } dragg_mpc_problem;
 
 typedef struct dragg_mpc_hash {
@@ -207,9 +210,10 @@ int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, 
                         void* stream);
 
 /* The keyed season-noise stream used when noise == NULL: writes [H][N] normals for
-   timestep t (exposed so the host and tests can reproduce the draw). */
+   timestep t (exposed so the host and tests can reproduce the draw); home i of the shard
+   draws the stream of global home home_offset + i*home_stride (home_stride 0 = 1). */
 int dragg_mpc_season_noise(const dragg_mpc_dims* dims, uint64_t seed, int32_t home_offset,
-                           int32_t timestep, double* noise_out, void* stream);
+                           int32_t home_stride, int32_t timestep, double* noise_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,15 +12,16 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from dragg_amd.aggregator import DeviceAggregator, shard_bounds
+from dragg_amd.aggregator import DeviceAggregator, shard_index
 
 
 class FakeBatch:
     """Deterministic stand-in: each home contributes (index+1)*t to the three sums."""
 
-    def __init__(self, homes, *a, home_offset=0, device=None, **kw):
+    def __init__(self, homes, *a, home_offset=0, home_stride=1, device=None, **kw):
         self.N, self.H = len(homes), 4
-        self.off = home_offset
+        self.off, self.stride = home_offset, home_stride
+        self.gidx = home_offset + home_stride * torch.arange(self.N, dtype=torch.float64)   # global indices
         self.t = 0
         self.status = torch.zeros(self.N, dtype=torch.int32)
         self.iters = torch.zeros(self.N, dtype=torch.int32)
@@ -30,11 +31,10 @@ class FakeBatch:
         self.t = t
         if hist is not None:
             hist.zero_()
-            hist[0] = torch.arange(self.off, self.off + self.N, dtype=torch.float64)
+            hist[0] = self.gidx
 
     def aggregate(self):
-        idx = torch.arange(self.off, self.off + self.N, dtype=torch.float64) + 1
-        s = float(idx.sum()) * self.t
+        s = float((self.gidx + 1).sum()) * self.t
         return torch.tensor([s, 2 * s, 3 * s], dtype=torch.float64)
 
 
@@ -57,7 +57,7 @@ def _worker(rank, world, port, n, steps, q):
     for _ in range(steps):
         agg.run_iteration()
         out.append(agg.collect_data().tolist())
-    q.put((rank, agg.lo, agg.hi, out, agg.hist[:, 0, :].tolist()))
+    q.put((rank, agg.index.tolist(), out, agg.hist[:, 0, :].tolist()))
     dist.destroy_process_group()
 
 
@@ -73,21 +73,21 @@ def test_two_rank_allreduce_and_sharding(n):
     res = sorted(q.get(timeout=120) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    # contiguous, disjoint, covering shards
-    assert res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == n
+    # strided, disjoint, covering shards
+    assert sorted(res[0][1] + res[1][1]) == list(range(n)) and res[1][1] == list(range(1, n, 2))
     total = sum(range(1, n + 1))
-    for rank, lo, hi, out, hist in res:
+    for rank, idx, out, hist in res:
         for t, v in enumerate(out):
             assert v == [total * t, 2 * total * t, 3 * total * t]      # all-reduced sums, every rank
-        assert hist[0] == list(map(float, range(lo, hi)))              # global home indices
+        assert hist[0] == list(map(float, idx))                        # global home indices
 
 
-def test_shard_bounds_cover():
+def test_shard_index_cover():
     for n in range(0, 40):
         for w in (1, 2, 3, 8):
-            parts = [shard_bounds(n, r, w) for r in range(w)]
-            assert parts[0][0] == 0 and parts[-1][1] == n
-            assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+            parts = [shard_index(n, r, w).tolist() for r in range(w)]
+            assert sorted(sum(parts, [])) == list(range(n))
+            assert max(map(len, parts)) - min(map(len, parts)) <= 1          # balanced counts
 
 
 # ------------------------------------------------------------------ the runner over 2 ranks
@@ -97,7 +97,7 @@ class HashBatch(FakeBatch):
     def step(self, t, noise=None, hist=None):
         self.t = t
         if hist is not None:
-            v = torch.arange(self.off, self.off + self.N, dtype=torch.float64) + 100.0 * t
+            v = self.gidx + 100.0 * t
             hist.copy_(v.expand_as(hist))
 
 
@@ -109,12 +109,12 @@ def _runner_worker(rank, world, port, root, q):
     a = Aggregator(data_dir=os.path.join(root, "data"), outputs_dir=os.path.join(root, "outputs"),
                    device=torch.device("cpu"), batch_cls=HashBatch)
     path = a.run()
-    q.put((rank, a.dev.lo, a.dev.hi, path))
+    q.put((rank, a.dev.index.tolist(), path))
     dist.destroy_process_group()
 
 
 def test_runner_two_ranks_gathers_history(tmp_path):
-    """Two ranks each solve a contiguous shard; rank 0 gathers the hash history and writes
+    """Two ranks each solve a strided shard; rank 0 gathers the hash history and writes
     results.json with every home's series in community order."""
     import json
     from tests import fixtures as F
@@ -135,8 +135,8 @@ def test_runner_two_ranks_gathers_history(tmp_path):
     res = sorted(q.get(timeout=180) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert res[1][3] is None and res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == 7
-    with open(res[0][3]) as f:
+    assert res[1][2] is None and res[0][1] == [0, 2, 4, 6] and res[1][1] == [1, 3, 5]
+    with open(res[0][2]) as f:
         out = json.load(f)
     names = [k for k in out if k != "Summary"]
     assert len(names) == 7

@@ -30,11 +30,12 @@ def test_device_noise_matches_host(gpu):
     from dragg_amd.community import synthetic_homes
     from dragg_amd.mpc import MPCBatch
     homes = synthetic_homes(10, seed=1, days=2)
-    b = MPCBatch(homes, seed=0x1234567890ABCDEF, home_offset=100)
-    z = b.season_noise(7).cpu().numpy()
-    for i in range(10):
-        ref = _noise_host(0x1234567890ABCDEF, 100 + i, 7, b.H)
-        assert np.allclose(z[:, i], ref, rtol=0, atol=1e-13)
+    for stride in (1, 3):                  # contiguous and strided shards (shard_index)
+        b = MPCBatch(homes, seed=0x1234567890ABCDEF, home_offset=100, home_stride=stride)
+        z = b.season_noise(7).cpu().numpy()
+        for i in range(10):
+            ref = _noise_host(0x1234567890ABCDEF, 100 + stride * i, 7, b.H)
+            assert np.allclose(z[:, i], ref, rtol=0, atol=1e-13)
 
 
 def _c1_batch(int_mode="round"):
@@ -118,22 +119,26 @@ def test_aggregate_sums(gpu):
 
 
 def test_device_aggregator_shard_invariance(gpu):
-    """Homes split over two shards (as over two GPUs) give the same per-home results as one
-    batch: the season noise is keyed by the global home index."""
+    """Homes split over two or three strided shards (as over GPUs) give the same per-home
+    results as one batch: the season noise is keyed by the global home index."""
     import torch
     from dragg_amd.aggregator import DeviceAggregator
     d = F.load("c1_h24")
     env = d["env"]
     args = (d["homes"], env["oat"], env["ghi"], env["tou_window"], 0, 6)
     full = DeviceAggregator(*args, reward_price=[0.0] * 24, seed=9)
-    parts = [DeviceAggregator(*args, reward_price=[0.0] * 24, seed=9, rank=r, world=2) for r in range(2)]
-    for t in range(6):
-        full.run_iteration()
-        for p in parts:
-            p.run_iteration()
-    torch.cuda.synchronize()
-    joined = torch.cat([p.hist[:6] for p in parts], dim=2)
-    assert torch.equal(torch.nan_to_num(full.hist[:6], 7.0), torch.nan_to_num(joined, 7.0))
+    for w in (2, 3):
+        parts = [DeviceAggregator(*args, reward_price=[0.0] * 24, seed=9, rank=r, world=w) for r in range(w)]
+        for t in range(6):
+            if w == 2:
+                full.run_iteration()
+            for p in parts:
+                p.run_iteration()
+        torch.cuda.synchronize()
+        joined = torch.empty_like(full.hist[:6])
+        for r, p in enumerate(parts):
+            joined[:, :, r::w] = p.hist[:6]
+        assert torch.equal(torch.nan_to_num(full.hist[:6], 7.0), torch.nan_to_num(joined, 7.0))
 
 
 def test_per_home_facade_matches_batch(gpu):

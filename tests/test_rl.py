@@ -106,8 +106,8 @@ class PriceBatch:
     home's vals[0]; the sums are vals[0] and its square.  Enough to see whether a rollout
     leaks state and whether every rank got the broadcast price."""
 
-    def __init__(self, homes, *a, home_offset=0, device=None, **kw):
-        self.N, self.H, self.off = len(homes), 4, home_offset
+    def __init__(self, homes, *a, home_offset=0, home_stride=1, device=None, **kw):
+        self.N, self.H, self.off, self.stride = len(homes), 4, home_offset, home_stride
         self.vals = torch.zeros((19, self.N), dtype=torch.float64)
         self.fc = torch.zeros((15, self.H, self.N), dtype=torch.float64)
         self.status = torch.zeros(self.N, dtype=torch.int32)
@@ -117,7 +117,7 @@ class PriceBatch:
         self.rp = rp.clone()
 
     def step(self, t, noise=None, hist=None):
-        idx = torch.arange(self.off, self.off + self.N, dtype=torch.float64) + 1
+        idx = self.off + self.stride * torch.arange(self.N, dtype=torch.float64) + 1
         self.vals[0] += idx * (1 + float(self.rp[0])) * (t + 1)
         self.fc[0, 0] = self.vals[0]
         if hist is not None:
