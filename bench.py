@@ -115,9 +115,10 @@ def bytes_per_launch(batch, success_frac):
     return rd + wr + env
 
 
-def measured_traffic(workload_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes of this workload
-    (profiles/*/traffic.json: FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM)."""
+def measured_pmc(workload_key):
+    """The committed rocprofv3 PMC passes of this workload (profiles/*/traffic.json): HBM
+    bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) and the SQ
+    counters per launch."""
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")), reverse=True):
         try:
@@ -126,8 +127,13 @@ def measured_traffic(workload_key):
         except (OSError, ValueError):
             continue
         if tj.get("workload") == workload_key:
-            return tj.get("bytes_per_launch"), os.path.relpath(f, ROOT)
-    return None, None
+            return tj, os.path.relpath(f, ROOT)
+    return {}, None
+
+
+# VALU issue peak: a wave64 VALU instruction (fp64 FMA included) occupies its SIMD 4 cycles;
+# 256 CUs x 4 SIMDs at 2.4 GHz (MI355X_MICROARCH.md) -> wave-instructions per second
+VALU_PEAK = 256 * 4 * 2.4e9 / 4
 
 
 def traffic_key(n_total, H, dt, month, int_mode, world):
@@ -218,7 +224,9 @@ def main():
                         f"timestep(s) + the committed {60 // dt}-min step, H={H} ({Hh} h), month {args.month}, "
                         f"run_rl_agg, int_mode={args.int_mode}")
         achieved = bytes_per_launch(agg.batch, success) / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = measured_traffic(traffic_key(n_total, H, dt, args.month, args.int_mode, world))
+        pmc, traffic_src = measured_pmc(traffic_key(n_total, H, dt, args.month, args.int_mode, world))
+        traffic = pmc.get("bytes_per_launch")
+        valu = pmc.get("sq_per_launch", {}).get("SQ_INSTS_VALU")
         out = {
             "metric": "home-MPC solves/sec (homes x steps)", "value": value, "unit": "solves/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -236,6 +244,13 @@ def main():
                          "traffic_bytes_per_launch": traffic, "traffic_source": traffic_src,
                          "kernel": f"mpc_{'direct' if args.int_mode == 'round' else 'home'}_kernel",
                          "kernel_ms": kern_ms},
+            # the bound that does limit the kernel: VALU issue.  Achieved =
+            # VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU, committed pass of this
+            # workload) / the launch time measured here
+            "roofline_valu": ({"bound": "valu-issue", "achieved": valu / (kern_ms * 1e-3) / 1e9,
+                               "peak": VALU_PEAK / 1e9, "unit": "G wave-instr/s",
+                               "frac": valu / (kern_ms * 1e-3) / VALU_PEAK, "valu_per_launch": valu,
+                               "source": traffic_src} if valu else None),
             "cpu_baseline": cpu,
             "status_counts": stat_counts,
         }

@@ -1837,17 +1837,14 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
             L.par[k * NB_CAP + j] = (uint16_t)p;
             if (more) L.tarr[j] = key(out, blo1 + j, An, r1, c1);
         };
-        for (int j = jin0 + lane; j <= jin1; j += 2 * nt) {
-            const int j2 = min(j + nt, jin1);              // second target (a repeat past the end)
-            double bc1, bc2;
-            int bu1, bu2;
-            pick(j, bc1, bu1);
-            pick(j2, bc2, bu2);
-            const int i1 = win(j, bu1), i2 = win(j2, bu2);
-            const double2 s1 = L.rmin[i1], s2 = L.rmin[i2];
-            const int r1s = L.rsrc[i1], r2s = L.rsrc[i2];
-            emit(j, bc1, bu1, s1, r1s);
-            if (j + nt <= jin1) emit(j2, bc2, bu2, s2, r2s);
+        // one target per lane and pass: with the tournament pick a target's chain is short, and
+        // pairing targets (more registers, a clamped repeat past the end) measured slower
+        for (int j = jin0 + lane; j <= jin1; j += nt) {
+            double bc;
+            int bu;
+            pick(j, bc, bu);
+            const int wi = win(j, bu);
+            emit(j, bc, bu, L.rmin[wi], L.rsrc[wi]);
         }
         // boundary buckets: the first cheapest of their per-duty candidates
         for (int q = lane; q < nbnd; q += nt) {

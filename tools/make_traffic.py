@@ -2,7 +2,9 @@
 """profiles/<round>/traffic.json from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
 tools/gpu_profile.sh: HBM bytes per launch of the solver kernel = (2 x FETCH_SIZE +
 WRITE_SIZE) x 1024 (MI355X_MICROARCH.md §HBM: FETCH_SIZE counts half of a streaming read on
-gfx950; our reads are narrow, so the factor is an upper estimate)."""
+gfx950; our reads are narrow, so the factor is an upper estimate).  Also the SQ counters of
+the sq1 / sq2 passes per launch (VALU/LDS/SALU instruction counts, wave cycles in quad-cycles),
+from which bench.py prices the kernel against the VALU issue rate."""
 import argparse
 import csv
 import json
@@ -41,6 +43,15 @@ def main():
            "fetch_size_kb_per_launch": fetch, "write_size_kb_per_launch": write,
            "bytes_per_launch": (2.0 * fetch + write) * 1024.0,
            "formula": "(2 x FETCH_SIZE + WRITE_SIZE) x 1024, rocprofv3 --pmc, separate passes"}
+    sq = {}
+    for p in ("sq1", "sq2"):
+        f = os.path.join(a.prof, p, f"{p}_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        for c in sorted({r["Counter_Name"] for r in csv.DictReader(open(f))}):
+            sq[c] = per_dispatch(f, c, a.kernel)[0]
+    if sq:
+        out["sq_per_launch"] = sq
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
