@@ -161,9 +161,17 @@ def main():
 
     import torch
     from dragg_amd.aggregator import DeviceAggregator
+    # one rank per GPU over RCCL (backend "nccl").  DRAGG_BENCH_BACKEND=gloo rehearses the
+    # multi-rank path with several ranks on fewer GPUs (ranks share devices round-robin)
+    backend = os.environ.get("DRAGG_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
     agg = DeviceAggregator(homes, oat, ghi, tou, 0, total_steps, reward_price=[0.0],
                            int_mode=args.int_mode, seed=12, rank=rank, world=world, keep_history=False)
     stream = torch.cuda.current_stream()
@@ -188,7 +196,9 @@ def main():
         if rl:
             action(k)
         agg.run_iteration()
-        agg.collect_data()
+        agg.collect_data(defer=not rl)
+    if not rl:
+        agg.reduce_history()
     barrier()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
@@ -201,7 +211,9 @@ def main():
         if rl:
             agg.collect_data().tolist()         # the agent reads the community sums on the host
         else:
-            agg.collect_data()
+            agg.collect_data(defer=True)        # run_rbo_mpc: no feedback, one reduction at the end
+    if not rl:
+        agg.reduce_history()
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:

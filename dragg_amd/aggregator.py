@@ -52,6 +52,7 @@ class DeviceAggregator:
                      if keep_history else None)
         self.agg_hist = torch.zeros((num_timesteps, 3), dtype=torch.float64, device=dev)
         self.status_hist = torch.zeros((num_timesteps, n), dtype=torch.int8, device=dev)
+        self._deferred = []          # steps whose agg_hist row holds this rank's sums only
 
     # aggregator.py:711-726
     def run_iteration(self, noise=None):
@@ -62,21 +63,38 @@ class DeviceAggregator:
         self.timestep += 1
 
     # aggregator.py:728-755 (sums only; the per-home series stay in self.hist)
-    def collect_data(self):
+    def collect_data(self, defer=False):
+        """The step's [agg_load, forecast_load, agg_cost].  defer=True: nothing reads the
+        community sums before the run ends (run_rbo_mpc has no feedback, aggregator.py:757-778),
+        so this rank keeps its own sums and reduce_history() all-reduces every deferred step in
+        one collective; the ranks then need not meet at every step."""
         t = self.timestep - 1
         agg = self.batch.aggregate()
         if self.world > 1:
-            torch.distributed.all_reduce(agg, group=self.group)
+            if defer:
+                self._deferred.append(t)
+            else:
+                torch.distributed.all_reduce(agg, group=self.group)
         self.agg_hist[t].copy_(agg)
         return agg
+
+    def reduce_history(self):
+        """All-reduce the deferred steps' sums (one RCCL call); agg_hist is then community-wide."""
+        if self._deferred:
+            idx = torch.tensor(self._deferred, dtype=torch.long, device=self.agg_hist.device)
+            rows = self.agg_hist.index_select(0, idx)
+            torch.distributed.all_reduce(rows, group=self.group)
+            self.agg_hist.index_copy_(0, idx, rows)
+            self._deferred = []
+        return self.agg_hist[:self.timestep]
 
     # aggregator.py:757-778
     def run_baseline(self, steps=None, noise_fn=None):
         steps = self.num_timesteps - self.timestep if steps is None else steps
         for _ in range(steps):
             self.run_iteration(noise_fn(self.timestep) if noise_fn else None)
-            self.collect_data()
-        return self.agg_hist[:self.timestep]
+            self.collect_data(defer=True)
+        return self.reduce_history()
 
     # ------------------------------------------------------------------ RL reward-price path
     # (SURVEY.md §8 F4; aggregator.py:664-675, 876-896).  A step reads exactly three things

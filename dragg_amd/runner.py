@@ -113,10 +113,11 @@ class Aggregator:
         for t in range(self.num_timesteps):
             noise = noise_fn(t)[:, self.dev.index] if noise_fn is not None else None
             self.dev.run_iteration(noise)
-            self.dev.collect_data()
+            self.dev.collect_data(defer=True)      # no feedback: the sums are reduced at the end
             self.timestep = t + 1
             if (t + 1) % self.checkpoint_interval == 0:
                 self.write_outputs()
+        self.dev.reduce_history()
         self.dev.check_errors()
 
     # ------------------------------------------------------------------ RL aggregator (§8 F4)

@@ -53,11 +53,19 @@ def _worker(rank, world, port, n, steps, q):
     homes = [{"name": f"h{i}"} for i in range(n)]
     agg = DeviceAggregator(homes, None, None, None, 0, steps, rank=rank, world=world,
                            device=torch.device("cpu"), batch_cls=FakeBatch)
-    out = [agg.collect_data().tolist() for _ in range(0)]
+    out = []
     for _ in range(steps):
         agg.run_iteration()
         out.append(agg.collect_data().tolist())
-    q.put((rank, agg.index.tolist(), out, agg.hist[:, 0, :].tolist()))
+    # run_rbo_mpc's deferred sums: local per step, community-wide after reduce_history()
+    agg2 = DeviceAggregator(homes, None, None, None, 0, steps, rank=rank, world=world,
+                            device=torch.device("cpu"), batch_cls=FakeBatch)
+    local = []
+    for _ in range(steps):
+        agg2.run_iteration()
+        local.append(agg2.collect_data(defer=True).tolist())
+    deferred = agg2.reduce_history().tolist()
+    q.put((rank, agg.index.tolist(), out, agg.hist[:, 0, :].tolist(), local, deferred))
     dist.destroy_process_group()
 
 
@@ -76,9 +84,12 @@ def test_two_rank_allreduce_and_sharding(n):
     # strided, disjoint, covering shards
     assert sorted(res[0][1] + res[1][1]) == list(range(n)) and res[1][1] == list(range(1, n, 2))
     total = sum(range(1, n + 1))
-    for rank, idx, out, hist in res:
+    for rank, idx, out, hist, local, deferred in res:
+        mine = sum(i + 1 for i in idx)
         for t, v in enumerate(out):
             assert v == [total * t, 2 * total * t, 3 * total * t]      # all-reduced sums, every rank
+            assert local[t] == [mine * t, 2 * mine * t, 3 * mine * t]  # deferred: this shard's
+            assert deferred[t] == v                                    # one reduction at the end
         assert hist[0] == list(map(float, idx))                        # global home indices
 
 
