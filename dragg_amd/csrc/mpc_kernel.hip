@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <limits.h>
 #include <stdlib.h>
 
 #include "../../include/dragg_mi355x.h"
@@ -1675,8 +1676,20 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         zz = fmin(fmax(zz, fb), fb + 0.999999);
         return (int16_t)floor(A * zz);
     };
+    // key hull of the finite labels [kfl, kfh]: the next stage's targets b = key + sh*u
+    // (u in 0..S) outside its reach have no candidate, so the window is clipped to it (one
+    // wave; the tank chain's labels sit in a narrow band of its box).  Bit-identical: only
+    // empty buckets are dropped and the order of the kept ones is unchanged.
+    int kfl = INT_MIN / 2, kfh = INT_MAX / 2;
+    const bool clip = nt == WAVE;
     if (H > 1) {
-        for (int s = lane; s < nbz; s += nt) L.tarr[s] = key(lab[s], blo + s, L.cA[1], L.rt[1], c);
+        int hl = INT_MAX, hh = INT_MIN;
+        for (int s = lane; s < nbz; s += nt) {
+            const int T = key(lab[s], blo + s, L.cA[1], L.rt[1], c);
+            L.tarr[s] = T;
+            if (lab[s].x < BIG) { hl = min(hl, T); hh = max(hh, T); }
+        }
+        if (clip) { kfl = dpp_imin(hl); kfh = dpp_imax(hh); }
         __syncthreads();
     }
     for (int k = 1; k < H; ++k) {
@@ -1688,7 +1701,13 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         // the exact box test.
         const double c1 = Ak * c;
         int blo1;
-        const int nbz1 = window(k, c1, &blo1);
+        int nbz1 = window(k, c1, &blo1);
+        if (clip) {
+            const int lo1 = max(blo1, kfl + min(0, sh * S)), hi1 = min(blo1 + nbz1 - 1, kfh + max(0, sh * S));
+            if (lo1 > hi1) return 0;                      // no finite label can go on
+            blo1 = lo1;
+            nbz1 = hi1 - lo1 + 1;
+        }
         const double r1 = L.rt[k + 1];
         int jin0 = (int)ceil((tl - r1) * iw + c1 + 1e-6) - blo1;
         int jin1 = (int)floor((th - r1) * iw + c1 - 1e-6) - 1 - blo1;
@@ -1826,6 +1845,7 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
         };
         // run-minimum index of the winning duty (a valid index when there is none)
         auto win = [&](int j, int bu) { return min(max(blo1 + j - mlo + 1 - sh * max(bu, 0), 0), M + 2); };
+        int hl = INT_MAX, hh = INT_MIN;                   // key hull of this stage's finite labels
         auto emit = [&](int j, double bc, int bu, double2 src, int rs) {
             double2 out = make_double2(BIG, 0.0);
             int p = 0xFFFF;
@@ -1835,7 +1855,12 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
             }
             lab[j] = out;
             L.par[k * NB_CAP + j] = (uint16_t)p;
-            if (more) L.tarr[j] = key(out, blo1 + j, An, r1, c1);
+            if (more) {
+                const int T = key(out, blo1 + j, An, r1, c1);
+                L.tarr[j] = T;
+                hl = bu >= 0 ? min(hl, T) : hl;
+                hh = bu >= 0 ? max(hh, T) : hh;
+            }
         };
         // one target per lane and pass: with the tournament pick a target's chain is short, and
         // pairing targets (more registers, a clamped repeat past the end) measured slower
@@ -1871,8 +1896,14 @@ DEV int dp_zspace(const Home& h, LdsD& L, int lane, int nt, double g, double x0,
             const double2 out = make_double2(B.c, B.x);
             lab[j] = out;
             L.par[k * NB_CAP + j] = (uint16_t)B.p;
-            if (more) L.tarr[j] = key(out, blo1 + j, An, r1, c1);
+            if (more) {
+                const int T = key(out, blo1 + j, An, r1, c1);
+                L.tarr[j] = T;
+                hl = B.p != 0xFFFF ? min(hl, T) : hl;
+                hh = B.p != 0xFFFF ? max(hh, T) : hh;
+            }
         }
+        if (clip && more) { kfl = dpp_imin(hl); kfh = dpp_imax(hh); }
         __syncthreads();
         blo = blo1; nbz = nbz1; c = c1;
     }
