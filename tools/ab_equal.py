@@ -18,10 +18,10 @@ def dump(a):
     import torch
     from dragg_amd.aggregator import DeviceAggregator
     from dragg_amd.community import synthetic_homes, synthetic_weather
-    sim_hours = math.ceil(a.steps / 4)
+    sim_hours = math.ceil(a.steps / a.dt)
     days = math.ceil((sim_hours + a.horizon_hours + 2) / 24) + 1
-    homes = synthetic_homes(a.homes, seed=12, days=days, dt=4, horizon_hours=a.horizon_hours)
-    oat, ghi, tou = synthetic_weather(days, 4, sim_hours, seed=3, month=a.month)
+    homes = synthetic_homes(a.homes, seed=12, days=days, dt=a.dt, horizon_hours=a.horizon_hours)
+    oat, ghi, tou = synthetic_weather(days, a.dt, sim_hours, seed=3, month=a.month)
     agg = DeviceAggregator(homes, oat, ghi, tou, 0, a.steps, reward_price=[0.0], int_mode="round", seed=12)
     out = {}
     for t in range(a.steps):
@@ -59,6 +59,7 @@ if __name__ == "__main__":
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--horizon-hours", type=int, default=12)
     ap.add_argument("--month", type=int, default=7)
+    ap.add_argument("--dt", type=int, default=4)
     a = ap.parse_args()
     if a.compare:
         sys.exit(0 if compare(*a.compare) else 1)
