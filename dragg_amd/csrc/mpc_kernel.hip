@@ -1443,18 +1443,34 @@ DEV Lds lp_view(const LdsD& D) {
 
 // Exact interval feasibility of the T and E chains and the outer test of the Tw chain:
 // presolve_infeasible of the LP path, on the direct path's inputs.
-DEV bool presolve_direct(const Home& h, const LdsD& L, double twlo0, double twhi0) {
+DEV bool presolve_direct(const Home& h, const LdsD& L, double twlo0, double twhi0, int lane) {
     if (!(h.Twmin <= h.Tw0 && h.Tw0 <= h.Twmax)) return true;          // temp_wh_ev[0] bounds
     double Tlo = h.T0, Thi = h.T0, Wlo = h.Tw0, Whi = h.Tw0, Elo = h.E0, Ehi = h.E0;
     const double gS = h.g * h.S;
+    // stage k's coefficients, one stage per lane (a division each, off the serial chain); the
+    // interval recursion then reads them with v_readlane (same expressions as the serial form)
+    const bool lanes = h.H <= WAVE;
+    double bq = 0.0, cq = 0.0, dq = 0.0;
+    const int wl = lane & (WAVE - 1);                 // every wave of the workgroup keeps a copy
+    if (lanes && wl < h.H) {
+        bq = L.oat[wl + 1] * h.iR * 3600 * h.inv_c;
+        const double df = L.draw[wl + 1] / h.V, rem = 1 - df, d15 = df * TAP;
+        cq = rem + (-rem * h.iRw) * 3600 * h.inv_w;
+        dq = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
+    }
     for (int k = 0; k < h.H; ++k) {
-        const double bk = L.oat[k + 1] * h.iR * 3600 * h.inv_c;
+        double bk, ck, dk;
+        if (lanes) {
+            bk = read_lane(bq, k); ck = read_lane(cq, k); dk = read_lane(dq, k);
+        } else {
+            bk = L.oat[k + 1] * h.iR * 3600 * h.inv_c;
+            const double df = L.draw[k + 1] / h.V, rem = 1 - df, d15 = df * TAP;
+            ck = rem + (-rem * h.iRw) * 3600 * h.inv_w;
+            dk = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
+        }
         double lo = h.aT * Tlo + bk + fmin(0.0, gS), hi = h.aT * Thi + bk + fmax(0.0, gS);
         Tlo = fmax(lo, h.Tmin); Thi = fmin(hi, h.Tmax);
         if (Tlo > Thi + TOL_P * (1 + fabs(Thi))) return true;
-        const double df = L.draw[k + 1] / h.V, rem = 1 - df, d15 = df * TAP;
-        const double ck = rem + (-rem * h.iRw) * 3600 * h.inv_w;
-        const double dk = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
         const double wlo = k == 0 ? twlo0 : h.Twmin, whi = k == 0 ? twhi0 : h.Twmax;
         const double w0 = k == 0 ? h.Tw0 : 0.0;
         lo = (k == 0 ? ck * w0 : ck * Wlo) + dk + h.e * Tlo;
@@ -2107,7 +2123,7 @@ __global__ __launch_bounds__(NT, 2) void mpc_direct_kernel(KArgs a) {   // 2 wav
         twlo0 = fmax(h.Twmin, h.Twmin - Kc);
         twhi0 = fmin(h.Twmax, h.Twmax - Kc);
     }
-    int status = presolve_direct(h, D, twlo0, twhi0) ? DRAGG_ST_INFEASIBLE : DRAGG_ST_OPTIMAL;
+    int status = presolve_direct(h, D, twlo0, twhi0, lane) ? DRAGG_ST_INFEASIBLE : DRAGG_ST_OPTIMAL;
     pf.mark(DRAGG_PH_SETUP);
     double obj = NAN;
     if (status == DRAGG_ST_OPTIMAL) {
