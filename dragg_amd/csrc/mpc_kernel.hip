@@ -1458,6 +1458,8 @@ DEV bool presolve_direct(const Home& h, const LdsD& L, double twlo0, double twhi
         cq = rem + (-rem * h.iRw) * 3600 * h.inv_w;
         dq = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
     }
+    const double edis = h.brate * (1.0 / h.etad) / h.dt, echg = h.brate * h.etac / h.dt;
+    bool bad = false;
     for (int k = 0; k < h.H; ++k) {
         double bk, ck, dk;
         if (lanes) {
@@ -1468,22 +1470,24 @@ DEV bool presolve_direct(const Home& h, const LdsD& L, double twlo0, double twhi
             ck = rem + (-rem * h.iRw) * 3600 * h.inv_w;
             dk = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
         }
+        // no early exit: the flags are or-ed (the result is the same, and the recursion has no
+        // branch waiting on each comparison)
         double lo = h.aT * Tlo + bk + fmin(0.0, gS), hi = h.aT * Thi + bk + fmax(0.0, gS);
         Tlo = fmax(lo, h.Tmin); Thi = fmin(hi, h.Tmax);
-        if (Tlo > Thi + TOL_P * (1 + fabs(Thi))) return true;
+        bad |= Tlo > Thi + TOL_P * (1 + fabs(Thi));
         const double wlo = k == 0 ? twlo0 : h.Twmin, whi = k == 0 ? twhi0 : h.Twmax;
         const double w0 = k == 0 ? h.Tw0 : 0.0;
         lo = (k == 0 ? ck * w0 : ck * Wlo) + dk + h.e * Tlo;
         hi = (k == 0 ? ck * w0 : ck * Whi) + dk + h.e * Thi + h.f * h.S;
         Wlo = fmax(lo, wlo); Whi = fmin(hi, whi);
-        if (Wlo > Whi + TOL_P * (1 + fabs(Whi))) return true;
+        bad |= Wlo > Whi + TOL_P * (1 + fabs(Whi));
         if (h.batt) {
-            lo = Elo - h.brate * (1.0 / h.etad) / h.dt; hi = Ehi + h.brate * h.etac / h.dt;
+            lo = Elo - edis; hi = Ehi + echg;
             Elo = fmax(lo, h.Emin); Ehi = fmin(hi, h.Emax);
-            if (Elo > Ehi + TOL_P * (1 + fabs(Ehi))) return true;
+            bad |= Elo > Ehi + TOL_P * (1 + fabs(Ehi));
         }
     }
-    return false;
+    return bad;
 }
 
 // --------------------------------------------------------------------------------------
