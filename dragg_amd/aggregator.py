@@ -44,7 +44,7 @@ class DeviceAggregator:
         # CPU (tests/test_distributed.py); the solver itself is MPCBatch (HIP, no fallback).
         self.batch = batch_cls(self.homes, oat, ghi, tou, start_index, reward_price, int_mode=int_mode,
                               seed=seed, home_offset=rank, home_stride=world, max_iter=max_iter, check_every=check_every,
-                              device=dev)
+                              device=dev, template_home=homes[0] if homes else None)
         self.num_timesteps = num_timesteps
         self.timestep = 0
         n = self.batch.N

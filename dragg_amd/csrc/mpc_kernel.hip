@@ -2309,6 +2309,8 @@ int dragg_mpc_step(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob, dr
                    dragg_mpc_out* out, int32_t timestep, const double* noise, void* stream) {
     int rc = check_dims(dims);
     if (rc) return rc;
+    // an empty shard (more ranks than homes) is a no-op; its per-home arrays may be NULL
+    if (dims->n_homes == 0) return (prob && hash && out && timestep >= 0) ? DRAGG_OK : DRAGG_E_ARG;
     if (!prob || !hash || !out || timestep < 0 || !prob->params || !prob->home_type || !prob->oat ||
         !prob->ghi || !prob->tou || !prob->reward_price || !prob->draw_hourly || !hash->vals || !hash->fc ||
         !out->status || !out->iters || !out->obj || !out->relax_obj)
@@ -2327,6 +2329,7 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
                              void* stream) {
     int rc = check_dims(dims);
     if (rc) return rc;
+    if (dims->n_homes == 0) return (prob && in && hash && out) ? DRAGG_OK : DRAGG_E_ARG;
     if (!prob || !in || !hash || !out || !prob->params || !prob->home_type || !in->t || !in->T0 ||
         !in->Tw0 || !in->E0 || !in->counter || !in->winter || !in->draw || !in->oat || !in->ghi ||
         !in->price || !hash->vals || !hash->fc || !out->status || !out->iters || !out->obj ||
@@ -2339,7 +2342,8 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
 }
 
 int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, double* out3, void* stream) {
-    if (!dims || !hash || !hash->vals || !out3 || dims->n_homes < 0) return DRAGG_E_ARG;
+    // n_homes == 0: the sums are zero (vals may be NULL)
+    if (!dims || !hash || (!hash->vals && dims->n_homes > 0) || !out3 || dims->n_homes < 0) return DRAGG_E_ARG;
     hipLaunchKernelGGL(aggregate_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, hash->vals,
                        dims->n_homes, out3);
     return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
@@ -2347,9 +2351,10 @@ int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, 
 
 int dragg_mpc_season_noise(const dragg_mpc_dims* dims, uint64_t seed, int32_t home_offset, int32_t home_stride,
                            int32_t timestep, double* noise_out, void* stream) {
-    if (!dims || !noise_out || dims->n_homes < 0 || dims->horizon < 1) return DRAGG_E_ARG;
+    if (!dims || dims->n_homes < 0 || dims->horizon < 1) return DRAGG_E_ARG;
     const int total = dims->n_homes * ((dims->horizon + 1) / 2);
     if (total == 0) return DRAGG_OK;
+    if (!noise_out) return DRAGG_E_ARG;
     hipLaunchKernelGGL(noise_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                        dims->n_homes, dims->horizon, seed, home_offset, max(home_stride, 1), timestep, noise_out);
     return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;

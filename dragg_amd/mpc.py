@@ -30,21 +30,22 @@ def hems_dims(home):
     return S, dt, H, float(hems["discount_factor"])
 
 
-def pack_homes(homes):
+def pack_homes(homes, template=None):
     """home dicts (aggregator.py:423-449 schema) -> (params [NPARAM][N], types [N], draws [hours][N], dims).
 
     Derived constants are computed with the reference's own float expressions
-    (mpc_calc.py:157-189, 239-244, 257-258, 274)."""
+    (mpc_calc.py:157-189, 239-244, 257-258, 274).  `template`: a home of the community whose
+    hems settings give the dims of an empty shard (N = 0, more ranks than homes)."""
     N = len(homes)
-    if N == 0:
+    if N == 0 and template is None:
         raise ValueError("no homes")
-    S, dt, H, disc = hems_dims(homes[0])
+    S, dt, H, disc = hems_dims(homes[0] if N else template)
     for h in homes:
         if hems_dims(h) != (S, dt, H, disc):
             raise ValueError("all homes of a batch must share the hems settings (responsive_hems)")
     P = np.zeros((L.NPARAM, N))
     types = np.zeros(N, dtype=np.int32)
-    nd = max(len(h["wh"]["draw_sizes"]) for h in homes)
+    nd = max((len(h["wh"]["draw_sizes"]) for h in homes), default=1)
     draws = np.zeros((nd, N))
     for i, h in enumerate(homes):
         if h["type"] not in L.TYPE_CODE:
@@ -97,11 +98,13 @@ class MPCBatch:
     seed : key of the on-device season-noise stream used when no noise is supplied.
     home_offset, home_stride : global community index of home i is home_offset + i*home_stride
         (the season-noise key), so a shard draws the same numbers as the whole community.
+    template_home : a home of the community, for the dims of an empty shard (homes == []):
+        its steps are no-ops and its sums zero.
     """
 
     def __init__(self, homes, oat=None, ghi=None, tou=None, start_index=0, reward_price=(0.0,),
                  int_mode="round", seed=0, max_iter=4000, check_every=10, device="cuda", home_offset=0,
-                 home_stride=1):
+                 home_stride=1, template_home=None):
         if int_mode not in L.INT_MODES:
             raise ValueError(f"int_mode must be one of {sorted(L.INT_MODES)}, not {int_mode!r}")
         self.lib = L.load()
@@ -110,7 +113,7 @@ class MPCBatch:
         self.device = torch.device(device)
         self.homes = homes
         self.names = [h["name"] for h in homes]
-        P, types, draws, dm = pack_homes(homes)
+        P, types, draws, dm = pack_homes(homes, template_home)
         self.N, self.H, self.S, self.dt = len(homes), dm["H"], dm["S"], dm["dt"]
         dev = self.device
         self.params = torch.tensor(P, dtype=torch.float64, device=dev).contiguous()

@@ -107,7 +107,8 @@ enum dragg_int_mode {
 };
 
 typedef struct dragg_mpc_dims {
-    int32_t n_homes;       /* N                                                        */
+    int32_t n_homes;       /* N (0 = an empty shard: every entry point is a no-op,
+                              per-home pointers may be NULL; aggregate writes zeros)    */
     int32_t horizon;       /* H = prediction_horizon * dt            (mpc_calc.py:150) */
     int32_t sub_steps;     /* S = sub_subhourly_steps                (mpc_calc.py:148) */
     int32_t dt;            /* hourly_agg_steps                       (mpc_calc.py:149) */

@@ -69,9 +69,10 @@ def _worker(rank, world, port, n, steps, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [7, 10])
-def test_two_rank_allreduce_and_sharding(n):
-    world, steps = 2, 3
+@pytest.mark.parametrize("n,world", [(7, 2), (10, 2), (2, 3)])
+def test_two_rank_allreduce_and_sharding(n, world):
+    """(2, 3): more ranks than homes, rank 2's shard is empty and still joins every collective."""
+    steps = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -82,7 +83,7 @@ def test_two_rank_allreduce_and_sharding(n):
     for p in procs:
         p.join(timeout=60)
     # strided, disjoint, covering shards
-    assert sorted(res[0][1] + res[1][1]) == list(range(n)) and res[1][1] == list(range(1, n, 2))
+    assert sorted(sum((r[1] for r in res), [])) == list(range(n)) and res[1][1] == list(range(1, n, world))
     total = sum(range(1, n + 1))
     for rank, idx, out, hist, local, deferred in res:
         mine = sum(i + 1 for i in idx)
