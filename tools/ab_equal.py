@@ -47,6 +47,12 @@ def compare(p, q):
             bad += 1
             d = np.argwhere((x != y) & ~(np.isnan(x) & np.isnan(y))) if x.dtype == np.float64 else np.argwhere(x != y)
             print(f"{k}: {len(d)} entries differ, first {d[:3].tolist()}")
+            if k.startswith("obj"):               # approximation changes: objective shift of b vs a
+                t = k[3:]
+                ok = (A["st" + t] == 0) & (B["st" + t] == 0)
+                g = (y[ok] - x[ok]) / np.maximum(1.0, np.abs(x[ok]))
+                print(f"  {k}: (b - a)/max(1,|a|) over {ok.sum()} optimal: mean {g.mean():.2e} "
+                      f"max {g.max():.2e} min {g.min():.2e}")
     print("IDENTICAL" if bad == 0 else f"DIFFERENT in {bad} arrays")
     return bad == 0
 
