@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # DRAGG_LIB: an alternative build of the same library (kernel experiments); default in-tree
 LIB_PATH = os.environ.get("DRAGG_LIB") or os.path.join(HERE, "libdragg_mi355x.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # enums (mirror include/dragg_mi355x.h)
 BASE, PV_ONLY, BATTERY_ONLY, PV_BATTERY = 0, 1, 2, 3
@@ -63,7 +63,7 @@ class Hash(ctypes.Structure):
 
 class Out(ctypes.Structure):
     _fields_ = [("status", c_dp), ("iters", c_dp), ("obj", c_dp), ("relax_obj", c_dp), ("hist", c_dp),
-                ("cycles", c_dp)]
+                ("cycles", c_dp), ("int_path", c_dp)]
 
 
 class Explicit(ctypes.Structure):

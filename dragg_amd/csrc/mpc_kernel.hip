@@ -116,6 +116,7 @@ template <int CTRL, typename T>
 DEV T dpp_mov(T v) { return __builtin_amdgcn_update_dpp((T)0, v, CTRL, 0xf, 0xf, true); }
 // v_readlane on the 32-bit halves (the builtin takes an int: a double would be converted)
 DEV int read_lane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+DEV unsigned read_lane(unsigned v, int l) { return (unsigned)__builtin_amdgcn_readlane((int)v, l); }
 DEV double read_lane(double v, int l) {
     const long long b = __double_as_longlong(v);
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
@@ -1275,6 +1276,7 @@ DEV void write_missing(const KArgs& a, int home) {
     a.out.iters[home] = 0;
     a.out.obj[home] = NAN;
     a.out.relax_obj[home] = NAN;
+    if (a.out.int_path) a.out.int_path[home] = 0;
 }
 
 // --------------------------------------------------------------------------------------
@@ -1357,20 +1359,28 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
 constexpr int NB_CAP = 336;          // DP buckets per chain (config ranges need <= ~327 at any dt)
 constexpr int NBND = 8;              // box-boundary buckets per stage (dp_zspace; 4-5 in practice)
 
+constexpr int NF = NB_CAP;          // exact front DP: labels per stage (dp_front)
+constexpr int NTB = 256;             // key buckets and cost buckets per stage (dp_front)
+
 struct LdsD {
     double *draw, *oat, *ghi, *price;   // [H+1]
     double *x;                          // [8H] solution in the stage-slot layout of the LP path
     double *t2;                         // [H] p_grid (objective)
     double *cA, *cC, *cq;               // [H] coefficients of the chain being solved
-    double *rt;                         // [H+2] zero-duty reference trajectory of the chain
     double *sc;                         // [32] scalars / reduction scratch
     double *bx0, *bp1, *bp2;            // [H] battery: merged-domain origin, psi segment offsets
-    double2 *lab;                       // [NB_CAP] DP labels (cost, exact state)
-    double2 *rmin;                      // [NB_CAP+8] DP cheapest source label per key
-                                        //   (dp_fixed: its second label buffer)
+    double2 *lab;                       // [NB_CAP] DP labels (dp_front: front A (key, cost);
+                                        //   dp_zspace / dp_fixed: (cost, exact state))
+    double2 *rmin;                      // [NB_CAP+8] dp_front: front B; dp_zspace: cheapest
+                                        //   source label per key; dp_fixed: second label buffer
+    // --- tail, a union: dp_front's arrays or dp_zspace's (never live together)
+    unsigned long long *kb, *cb;        // [NTB]  dp_front: per key / cost bucket packed extremes
+    unsigned *mh, *kl;                  // [NTB]  dp_front: scans of kb / cb
+    float *flo, *fhi;                   // [H+1]  dp_front: feasible-set hull of x_k
     double2 *cand;                      // [NBND][S+1] boundary-bucket candidates per duty
-    int16_t *tarr, *rsrc;               // [NB_CAP], [NB_CAP+8] source keys, source of rmin
+    double *rt;                         // [H+2] zero-duty reference trajectory of the chain
     int *candp;                         // [NBND][S+1] candidate records
+    int16_t *tarr, *rsrc;               // [NB_CAP], [NB_CAP+8] source keys, source of rmin
     double *sgS, *sgL;                  // battery segments [2][seg_cap], in lab / rmin (the
                                         //   battery LP runs after the thermal DPs)
     uint16_t* par;                      // [H][NB_CAP] DP back-pointers (global workspace)
@@ -1386,47 +1396,95 @@ __host__ __device__ inline bool direct_compact(int H) {
 }
 __host__ __device__ inline bool direct_fits(int H) { return seg_cap(H) <= NB_CAP; }
 
-__host__ __device__ inline int direct_lds_bytes(int H, int S) {
-    int nd = 4 * (H + 1) + 8 * H + 3 * H + (H + 2) + 32 + 1 + 2 * NB_CAP + 2 * (NB_CAP + 8) + 2 * NBND * (S + 1);
-    if (!direct_compact(H)) nd += 4 * H;
-    return nd * 8 + (NB_CAP + NB_CAP + 8) * 2 + NBND * (S + 1) * 4;
+// Byte offsets of the direct kernel's LDS carve (one function for the device carve and the
+// host's launch size, so the two cannot disagree).
+// direct kernel workspace: [N][H][NB_CAP] u16 DP back-pointers, then [N][8H] f64 solutions
+__host__ __device__ inline size_t par_region_bytes(int N, int H) {
+    return ((size_t)N * H * NB_CAP * sizeof(uint16_t) + 255) / 256 * 256;
 }
 
-DEV LdsD carve_direct(double* s, int H, int S) {
-    LdsD L;
-    double* const base = s;
-    const bool compact = direct_compact(H);
-    L.draw = s; s += H + 1;
-    L.oat = s; s += H + 1;
-    L.ghi = s; s += H + 1;
-    L.price = s; s += H + 1;
-    L.x = s; s += 8 * H;
-    L.cA = s; s += H;
-    L.cC = s; s += H;
-    L.cq = s; s += H;
-    L.rt = s; s += H + 2;
-    L.sc = s; s += 32;
-    if (!compact) {
-        L.t2 = s; s += H;
-        L.bx0 = s; s += H;
-        L.bp1 = s; s += H;
-        L.bp2 = s; s += H;
+struct DirectLayout {
+    int draw, oat, ghi, price, cA, cC, cq, sc, t2, bx0, bp1, bp2, lab, rmin, tail;
+    int kb, cb, mh, kl, flo, fhi;             // dp_front tail
+    int cand, rt, candp, tarr, rsrc;          // dp_zspace tail
+    int bytes;
+};
+
+__host__ __device__ inline DirectLayout direct_layout(int H, int S) {
+    DirectLayout o{};
+    int p = 0;
+    auto take = [&](int bytes, int align) { p = (p + align - 1) / align * align; const int r = p; p += bytes; return r; };
+    o.draw = take(8 * (H + 1), 16);
+    o.oat = take(8 * (H + 1), 8);
+    o.ghi = take(8 * (H + 1), 8);
+    o.price = take(8 * (H + 1), 8);
+    o.cA = take(8 * H, 8);
+    o.cC = take(8 * H, 8);
+    o.cq = take(8 * H, 8);
+    o.sc = take(8 * 32, 8);
+    o.t2 = o.bx0 = o.bp1 = o.bp2 = -1;
+    if (!direct_compact(H)) {
+        o.t2 = take(8 * H, 8);
+        o.bx0 = take(8 * H, 8);
+        o.bp1 = take(8 * H, 8);
+        o.bp2 = take(8 * H, 8);
     }
-    if ((s - base) & 1) ++s;                                     // 16-B alignment of the labels
-    L.lab = reinterpret_cast<double2*>(s); s += 2 * NB_CAP;
-    L.rmin = reinterpret_cast<double2*>(s); s += 2 * (NB_CAP + 8);
-    L.cand = reinterpret_cast<double2*>(s); s += 2 * NBND * (S + 1);
-    L.tarr = reinterpret_cast<int16_t*>(s);
-    L.rsrc = L.tarr + NB_CAP;
-    L.candp = reinterpret_cast<int*>(L.rsrc + NB_CAP + 8);
+    o.lab = take(16 * NB_CAP, 16);
+    o.rmin = take(16 * (NB_CAP + 8), 16);
+    o.tail = p;
+    // dp_front tail
+    o.kb = take(8 * NTB, 16);
+    o.cb = take(8 * NTB, 16);
+    o.mh = take(4 * NTB, 4);
+    o.kl = take(4 * NTB, 4);
+    o.flo = take(4 * (H + 1), 4);
+    o.fhi = take(4 * (H + 1), 4);
+    const int end_front = p;
+    // dp_zspace tail (same origin)
+    p = o.tail;
+    o.cand = take(16 * NBND * (S + 1), 16);
+    o.rt = take(8 * (H + 2), 8);
+    o.candp = take(4 * NBND * (S + 1), 4);
+    o.tarr = take(2 * NB_CAP, 2);
+    o.rsrc = take(2 * (NB_CAP + 8), 2);
+    o.bytes = (max(end_front, p) + 15) / 16 * 16;
+    return o;
+}
+
+__host__ __device__ inline int direct_lds_bytes(int H, int S) { return direct_layout(H, S).bytes; }
+
+DEV LdsD carve_direct(double* smem, int H, int S) {
+    const DirectLayout o = direct_layout(H, S);
+    char* b = reinterpret_cast<char*>(smem);
+    auto D = [&](int off) { return reinterpret_cast<double*>(b + off); };
+    LdsD L;
+    L.draw = D(o.draw); L.oat = D(o.oat); L.ghi = D(o.ghi); L.price = D(o.price);
+    L.x = nullptr;                                               // global workspace (kernel)
+    L.cA = D(o.cA); L.cC = D(o.cC); L.cq = D(o.cq);
+    L.sc = D(o.sc);
+    L.lab = reinterpret_cast<double2*>(b + o.lab);
+    L.rmin = reinterpret_cast<double2*>(b + o.rmin);
+    L.kb = reinterpret_cast<unsigned long long*>(b + o.kb);
+    L.cb = reinterpret_cast<unsigned long long*>(b + o.cb);
+    L.mh = reinterpret_cast<unsigned*>(b + o.mh);
+    L.kl = reinterpret_cast<unsigned*>(b + o.kl);
+    L.flo = reinterpret_cast<float*>(b + o.flo);
+    L.fhi = reinterpret_cast<float*>(b + o.fhi);
+    L.cand = reinterpret_cast<double2*>(b + o.cand);
+    L.rt = D(o.rt);
+    L.candp = reinterpret_cast<int*>(b + o.candp);
+    L.tarr = reinterpret_cast<int16_t*>(b + o.tarr);
+    L.rsrc = reinterpret_cast<int16_t*>(b + o.rsrc);
     const int sc = seg_cap(H);
     L.sgS = reinterpret_cast<double*>(L.lab);
     L.sgL = reinterpret_cast<double*>(L.rmin);
-    if (compact) {
+    if (direct_compact(H)) {
         L.bx0 = L.sgS + 2 * sc;
         L.bp1 = L.bx0 + H;
         L.bp2 = L.bp1 + H;
         L.t2 = L.sgL + 2 * sc;
+    } else {
+        L.t2 = D(o.t2); L.bx0 = D(o.bx0); L.bp1 = D(o.bp1); L.bp2 = D(o.bp2);
     }
     L.par = nullptr;                                             // set by the kernel
     return L;
@@ -1976,6 +2034,282 @@ DEV bool dp_thermal(const Home& h, LdsD& L, int lane, int nt, double g, double x
 }
 
 // --------------------------------------------------------------------------------------
+// EXACT thermal chain DP: forward Pareto fronts (dp_front).
+//
+// Chain  x_{k+1} = A_k x_k + C_k + g u_k,  u_k in {0..S},  x_1 in [lo0, hi0],
+// x_{k+1} in [lo, hi] (k >= 1),  minimise sum_k q_k u_k  (q_k = gamma^k price_k P S:
+// mpc_calc.py:314-317, 330-332, 318-349, 441-446).
+//
+// Key s = dx * x oriented so that a larger key is "more duty done" when every q_k >= 0
+// (dx = sign g) and "less duty done" when every q_k <= 0 (dx = -sign g).  The cost-to-go
+// V_k(s) is then non-increasing in s on the set F_k of states that still have a feasible
+// continuation, so a label (s_a, c_a) with s_a >= s_b, c_a <= c_b makes (s_b, c_b) useless.
+// No bucketing approximation: every kept label carries its exact state and cost, and a
+// label is dropped only when another label provably dominates it.  Checked against an
+// assumption-free backward step-function DP (oracle/thermal.py) and HiGHS proven optima.
+//
+// F_k (states of stage k with a feasible continuation) is the hull of the box and the
+// preimage of F_{k+1} under the stage map; with F_{k+1} at least one duty step wide the
+// preimages of consecutive duties overlap, so the hull is exact (narrower: the caller falls
+// back).  Children outside F_{k+1} are dropped (they could dominate and then die).
+//
+// One stage on one wave; the front is an UNSORTED list (nothing needs its order):
+//  1. every child (parent i, duty u) inside F_{k+1} falls in one of NTB equal KEY buckets
+//     of the children's key range and one of NTB equal COST buckets of their cost range;
+//     64-bit LDS atomics keep per key bucket the cheapest child (largest key among equally
+//     cheap ones) and per cost bucket the largest-key child (cheapest among equal keys),
+//     as 32-bit ordered bounds rounded outward (cost up, key down);
+//  2. two wave scans: mh_b = min cost over the key buckets above b, kl_b = max key over
+//     the cost buckets below b;
+//  3. a child is dropped if one of these four references provably dominates it (its own
+//     key rounded up, cost rounded down): a key bucket above, its key bucket's cheapest
+//     child, a cost bucket below, its cost bucket's largest-key child.  Key buckets alone
+//     cannot separate labels of equal duty totals (a tank without draws: A = 1 - 4e-5, keys
+//     equal to 1e-5 while costs differ), cost buckets can;
+//  4. the others are appended (wave ballot, parent order) as the new front.
+// A dominated child that no reference catches is kept: that only costs work (measured:
+// fronts within 0.1-0.4 % of the exact Pareto fronts at NTB = 256).  Back-pointer (parent | duty << 12) per new label goes to the
+// global workspace.  Returns 1 solved (optimal for the chain), 0 no integer schedule, -1 not
+// applicable (mixed-sign prices, a feasible set narrower than one duty step, front
+// overflow): the caller falls back.
+// --------------------------------------------------------------------------------------
+struct FrontBufs {
+    double2 *fa, *fb;                    // [NF] fronts (key, cost), ping-pong
+    unsigned long long* kb;              // [NTB] key buckets: packed (cost up | ~key down) minima
+    unsigned long long* cb;              // [NTB] cost buckets: packed (key down | ~cost up) maxima
+    unsigned* mh;                        // [NTB] ordered min cost over the key buckets above
+    unsigned* kl;                        // [NTB] ordered max key over the cost buckets below
+    float *flo, *fhi;                    // [H + 1] feasible-set hull of x_k
+    const double *cA, *cC, *cq;          // [H] chain coefficients and duty costs
+    double* x;                           // [8H] stage-slot solution (writes slots sx, sv)
+    uint16_t* par;                       // [H][NB_CAP] global
+};
+
+DEV float f32_down(double v) { float f = (float)v; return (double)f > v ? nextafterf(f, -INFINITY) : f; }
+DEV float f32_up(double v) { float f = (float)v; return (double)f < v ? nextafterf(f, INFINITY) : f; }
+// floats -> u32 with the same order
+DEV unsigned ord32(float v) {
+    const unsigned b = __float_as_uint(v);
+    return (b >> 31) ? ~b : (b | 0x80000000u);
+}
+// inclusive scan over the 64 lanes with identity id (lanes shifted in from outside a row
+// keep id: bound_ctrl off), rows combined through v_readlane
+template <int CTRL, typename T>
+DEV T dpp_mov_or(T v, T id) { return __builtin_amdgcn_update_dpp(id, v, CTRL, 0xf, 0xf, false); }
+template <typename T, typename Op>
+DEV T dpp_iscan(T v, int lane, T id, Op op) {
+    v = op(v, dpp_mov_or<0x111>(v, id));
+    v = op(v, dpp_mov_or<0x112>(v, id));
+    v = op(v, dpp_mov_or<0x114>(v, id));
+    v = op(v, dpp_mov_or<0x118>(v, id));
+    const T t0 = read_lane(v, 15), t1 = read_lane(v, 31), t2 = read_lane(v, 47);
+    const int row = lane >> 4;
+    const T o1 = t0, o2 = op(t0, t1), o3 = op(o2, t2);
+    const T off = row == 1 ? o1 : row == 2 ? o2 : o3;
+    return row == 0 ? v : op(v, off);
+}
+
+template <int SS>
+DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, double lo0, double hi0, double lo,
+                 double hi, int sx, int sv) {
+    static_assert(SS > 0 && SS < 16, "duty count must be a compile-time constant below 16");
+    constexpr int NU = SS + 1;
+    constexpr int BPL = NTB / WAVE;      // buckets per lane in the scan
+    static_assert(NTB % WAVE == 0, "");
+    auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
+    auto umin = [](unsigned a, unsigned b) { return a < b ? a : b; };
+    auto umax = [](unsigned a, unsigned b) { return a > b ? a : b; };
+    // (a) sign of the duty costs: the orientation of the key
+    bool pos = false, neg = false;
+    for (int k = lane; k < H; k += WAVE) {
+        const double q = B.cq[k];
+        pos = pos || q > 0.0;
+        neg = neg || q < 0.0;
+    }
+    pos = __any(pos);
+    neg = __any(neg);
+    if (pos && neg) return -1;
+    const double dx = ((g > 0.0) != neg) ? 1.0 : -1.0;
+    // (b) feasible-set hulls F_H .. F_1 (every lane computes, lane 0 stores)
+    {
+        bool empty = false, narrow = false;
+        double l = H == 1 ? lo0 : lo, u = H == 1 ? hi0 : hi;
+        l -= tw(l);
+        u += tw(u);
+        if (lane == 0) { B.flo[H] = f32_down(l); B.fhi[H] = f32_up(u); }
+        const double gmin = fmin(0.0, g * SS), gmax = fmax(0.0, g * SS);
+        for (int k = H - 1; k >= 1 && !empty; --k) {
+            narrow = narrow || (u - l < fabs(g));
+            const double A = B.cA[k], C = B.cC[k];
+            const double pl = (l - C - gmax) / A, ph = (u - C - gmin) / A;
+            const double bl = k == 1 ? lo0 : lo, bh = k == 1 ? hi0 : hi;
+            l = fmax(pl, bl - tw(bl));
+            u = fmin(ph, bh + tw(bh));
+            l -= tw(l);
+            u += tw(u);
+            empty = l > u;
+            if (lane == 0) { B.flo[k] = f32_down(l); B.fhi[k] = f32_up(u); }
+        }
+        if (empty) return 0;
+        if (narrow) return -1;
+    }
+    double2* fa = B.fa;
+    double2* fb = B.fb;
+    if (lane == 0) fa[0] = make_double2(dx * x0, 0.0);
+    int n = 1;
+    double smin = dx * x0, smax = dx * x0, cmin = 0.0, cmax = 0.0;   // key / cost range of the front
+    const unsigned long long below = (1ull << lane) - 1ull;          // lanes < this one
+    for (int b = lane; b < NTB; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
+    __syncthreads();
+    for (int k = 0; k < H; ++k) {
+        const double A = B.cA[k], C = B.cC[k], q = B.cq[k];
+        double bl = k == 0 ? lo0 : lo, bh = k == 0 ? hi0 : hi;
+        bl -= tw(bl);
+        bh += tw(bh);
+        if (k + 1 < H) { bl = fmax(bl, (double)B.flo[k + 1]); bh = fmin(bh, (double)B.fhi[k + 1]); }
+        const double sl = dx > 0.0 ? bl : -bh, sh = dx > 0.0 ? bh : -bl;
+        // the children's key and cost ranges: the two bucket grids of this stage
+        const double D = dx * g;
+        const double klo = fmax(sl, dx * fma(A, dx * smin, C) + fmin(0.0, D * SS));
+        const double khi = fmin(sh, dx * fma(A, dx * smax, C) + fmax(0.0, D * SS));
+        if (!(klo <= khi)) return 0;                     // no child can stay feasible
+        const double clo = cmin + fmin(0.0, q * SS), chi = cmax + fmax(0.0, q * SS);
+        const double ikw = khi > klo ? (double)NTB / (khi - klo) : 0.0;
+        const double icw = chi > clo ? (double)NTB / (chi - clo) : 0.0;
+        auto kbucket = [&](double t) { return min(NTB - 1, max(0, (int)((t - klo) * ikw))); };
+        auto cbucket = [&](double c) { return min(NTB - 1, max(0, (int)((c - clo) * icw))); };
+        // 1. per key bucket the cheapest child (largest key among equally cheap ones), per
+        //    cost bucket the largest key (cheapest among equal keys); bounds rounded outward
+        //    (cost up, key down) so that every reference is no better than a real child
+        for (int i = lane; i < n; i += WAVE) {
+            const double2 Li = fa[i];
+            const double xi = dx * Li.x;
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const double t = dx * fma(A, xi, fma(g, (double)u, C));
+                if (t >= sl && t <= sh) {
+                    const double c = fma(q, (double)u, Li.y);
+                    const unsigned cu = ord32(f32_up(c)), kd = ord32(f32_down(t));
+                    atomicMin(&B.kb[kbucket(t)], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
+                    atomicMax(&B.cb[cbucket(c)], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
+                }
+            }
+        }
+        __syncthreads();
+        // 2. mh[b] = min cost over the key buckets above b (lane l holds key chunk 63 - l:
+        //    "above" = lower lanes, an exclusive prefix-min); kl[b] = max key over the cost
+        //    buckets below b (lane l holds cost chunk l: an exclusive prefix-max)
+        {
+            const int c0 = (WAVE - 1 - lane) * BPL, d0 = lane * BPL;
+            unsigned bm[BPL], bk[BPL];
+            unsigned lm = ~0u, lk = 0u;
+#pragma unroll
+            for (int j = 0; j < BPL; ++j) {
+                bm[j] = (unsigned)(B.kb[c0 + j] >> 32);
+                lm = umin(lm, bm[j]);
+                bk[j] = (unsigned)(B.cb[d0 + j] >> 32);
+                lk = umax(lk, bk[j]);
+            }
+            const unsigned im = dpp_iscan(lm, lane, ~0u, umin);
+            const unsigned ik = dpp_iscan(lk, lane, 0u, umax);
+            unsigned rm = __shfl_up(im, 1), rk = __shfl_up(ik, 1);
+            if (lane == 0) { rm = ~0u; rk = 0u; }
+#pragma unroll
+            for (int j = BPL - 1; j >= 0; --j) {
+                B.mh[c0 + j] = rm;
+                rm = umin(rm, bm[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < BPL; ++j) {
+                B.kl[d0 + j] = rk;
+                rk = umax(rk, bk[j]);
+            }
+        }
+        __syncthreads();
+        // 3. survivors appended to the other buffer in (parent, duty) order.  A child X is
+        //    dropped when some reference provably dominates it; X's own bounds are rounded
+        //    the other way (key up, cost down), so a dropped child is always dominated:
+        //    - a key bucket above holds a child no dearer:         cost_dn(X) >= mh
+        //    - its key bucket's cheapest child Y:   key_up(X) <= key(Y), cost_dn(X) >= cost(Y)
+        //    - a cost bucket below holds a child with no smaller key: key_up(X) <= kl
+        //    - its cost bucket's largest-key child Y' likewise
+        //    (the two per-bucket tests need one strict inequality: X may be the reference)
+        int nn = 0;
+        double nkmin = INFINITY, nkmax = -INFINITY, ncmin = INFINITY, ncmax = -INFINITY;
+        for (int p = 0; p * WAVE < n; ++p) {
+            const int i = lane + p * WAVE;
+            const bool have = i < n;
+            const double2 Li = have ? fa[i] : make_double2(0.0, 0.0);
+            const double xi = dx * Li.x;
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const double t = dx * fma(A, xi, fma(g, (double)u, C));
+                const double c = fma(q, (double)u, Li.y);
+                bool keep = have && t >= sl && t <= sh;
+                if (keep) {
+                    const int kbk = kbucket(t), cbk = cbucket(c);
+                    const unsigned ku = ord32(f32_up(t)), cd = ord32(f32_down(c));
+                    const unsigned long long ky = B.kb[kbk], cy = B.cb[cbk];
+                    const unsigned ycu = (unsigned)(ky >> 32), ykd = ~(unsigned)ky;
+                    const unsigned zkd = (unsigned)(cy >> 32), zcu = ~(unsigned)cy;
+                    const bool d1 = cd >= B.mh[kbk];
+                    const bool d2 = ku <= ykd && cd >= ycu && (ku < ykd || cd > ycu);
+                    const bool d3 = ku <= B.kl[cbk];
+                    const bool d4 = ku <= zkd && cd >= zcu && (ku < zkd || cd > zcu);
+                    keep = !(d1 || d2 || d3 || d4);
+                }
+                const unsigned long long bal = __ballot(keep);
+                const int slot = nn + __popcll(bal & below);
+                nn += __popcll(bal);
+                if (keep && slot < NF) {
+                    fb[slot] = make_double2(t, c);
+                    B.par[k * NB_CAP + slot] = (uint16_t)(i | (u << 12));
+                    nkmin = fmin(nkmin, t);
+                    nkmax = fmax(nkmax, t);
+                    ncmin = fmin(ncmin, c);
+                    ncmax = fmax(ncmax, c);
+                }
+            }
+        }
+        if (nn == 0) return 0;                       // no child left inside the feasible set
+        if (nn > NF) return -1;                      // front overflow
+        smin = dpp_reduce(nkmin, [](double a, double b) { return fmin(a, b); });
+        smax = dpp_reduce(nkmax, [](double a, double b) { return fmax(a, b); });
+        cmin = dpp_reduce(ncmin, [](double a, double b) { return fmin(a, b); });
+        cmax = dpp_reduce(ncmax, [](double a, double b) { return fmax(a, b); });
+        for (int b = lane; b < NTB; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
+        __syncthreads();
+        double2* tmp = fa; fa = fb; fb = tmp;
+        n = nn;
+    }
+    // the cheapest final label (lowest index on ties)
+    double best = INFINITY;
+    int bi = -1;
+    for (int i = lane; i < n; i += WAVE)
+        if (fa[i].y < best) { best = fa[i].y; bi = i; }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bi, o);
+        if (ob < best || (ob == best && oi >= 0 && (bi < 0 || oi < bi))) { best = ob; bi = oi; }
+    }
+    if (lane == 0) {
+        int j = bi;
+        for (int k = H - 1; k >= 0; --k) {
+            const int p = B.par[k * NB_CAP + j];
+            B.x[k * 8 + sv] = (double)(p >> 12);
+            j = p & 0xFFF;
+        }
+        double x = x0;                      // exact forward trajectory (the labels' arithmetic)
+        for (int k = 0; k < H; ++k) {
+            x = fma(B.cA[k], x, fma(g, B.x[k * 8 + sv], B.cC[k]));
+            B.x[k * 8 + sx] = x;
+        }
+    }
+    __syncthreads();
+    return 1;
+}
+
+// --------------------------------------------------------------------------------------
 // Battery LP (mpc_calc.py:355-373 with its p_grid / cost terms): min sum_k q_k (ch_k + dis_k),
 // E_{k+1} = E_k + a ch_k + b dis_k (a = eta_c/dt, b = 1/(eta_d dt)), 0 <= ch <= r,
 // -r <= dis <= 0, Emin <= E_{1..H} <= Emax, q_k = S gamma^k price_k.
@@ -2106,6 +2440,10 @@ __global__ __launch_bounds__(NT, 2) void mpc_direct_kernel(KArgs a) {   // 2 wav
     const int H = a.d.horizon;
     LdsD D = carve_direct(smem, H, a.d.sub_steps);
     D.par = reinterpret_cast<uint16_t*>(a.p.workspace) + (size_t)home * H * NB_CAP;
+    // the stage-slot solution lives in the workspace too (after every home's back-pointers):
+    // it is written once per chain and read by the cleanup, so LDS goes to the DP
+    D.x = reinterpret_cast<double*>(reinterpret_cast<char*>(a.p.workspace) + par_region_bytes(N, H)) +
+          (size_t)home * 8 * H;
     Lds L = lp_view(D);
     Io io{a.vals, a.fc, N, home};
     Prof pf;
@@ -2130,6 +2468,7 @@ __global__ __launch_bounds__(NT, 2) void mpc_direct_kernel(KArgs a) {   // 2 wav
     int status = presolve_direct(h, D, twlo0, twhi0, lane) ? DRAGG_ST_INFEASIBLE : DRAGG_ST_OPTIMAL;
     pf.mark(DRAGG_PH_SETUP);
     double obj = NAN;
+    int int_path = 0;
     if (status == DRAGG_ST_OPTIMAL) {
         // chain 0: indoor air (mpc_calc.py:314-317), u = duty of the season's mode (:303-309);
         // chain 1: water heater given T (mpc_calc.py:330-332).  One DP instantiation for both.
@@ -2156,8 +2495,20 @@ __global__ __launch_bounds__(NT, 2) void mpc_direct_kernel(KArgs a) {   // 2 wav
             const double lo0 = c0 ? h.Tmin : twlo0, hi0 = c0 ? h.Tmax : twhi0;
             const double lo = c0 ? h.Tmin : h.Twmin, hi = c0 ? h.Tmax : h.Twmax;
             const int sx = c0 ? S_T : S_TW, sv = c0 ? S_U : S_W;
-            ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
-                          : dp_thermal<0>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
+            // the exact front DP; the bucketed DP only where it does not apply (mixed-sign
+            // prices, a feasible set narrower than one duty step, front overflow, S != 6)
+            int r = -1;
+            if (NT == WAVE && h.S == 6) {
+                const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par};
+                r = dp_front<6>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv);
+            }
+            if (r >= 0) {
+                ok = r == 1;
+            } else {
+                int_path |= 1 << chain;
+                ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
+                              : dp_thermal<0>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
+            }
         }
         pf.mark(DRAGG_PH_INTEGER);
         if (!ok) status = DRAGG_ST_ROUND_FAIL;
@@ -2184,6 +2535,7 @@ __global__ __launch_bounds__(NT, 2) void mpc_direct_kernel(KArgs a) {   // 2 wav
         a.out.iters[home] = 0;
         a.out.obj[home] = obj;
         a.out.relax_obj[home] = NAN;
+        if (a.out.int_path) a.out.int_path[home] = int_path;
     }
     if (a.out.hist && lane == 0)      // lane 0 wrote every vals field of this home
         for (int k = 0; k < DRAGG_NVAL; ++k) a.out.hist[(size_t)k * N + home] = io.v(k);
@@ -2225,7 +2577,7 @@ __global__ void noise_kernel(int N, int H, uint64_t seed, int off, int stride, i
 bool direct_mode(const dragg_mpc_dims* d) { return d->int_mode == DRAGG_INT_ROUND; }
 
 size_t workspace_bytes(const dragg_mpc_dims* d) {
-    return direct_mode(d) ? (size_t)d->n_homes * d->horizon * NB_CAP * sizeof(uint16_t) : 0;
+    return direct_mode(d) ? par_region_bytes(d->n_homes, d->horizon) + (size_t)d->n_homes * 8 * d->horizon * 8 : 0;
 }
 
 size_t kernel_lds_bytes(const dragg_mpc_dims* d) {

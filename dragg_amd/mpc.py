@@ -136,6 +136,7 @@ class MPCBatch:
         self.iters = torch.zeros(self.N, dtype=torch.int32, device=dev)
         self.obj = torch.zeros(self.N, dtype=torch.float64, device=dev)
         self.relax_obj = torch.zeros(self.N, dtype=torch.float64, device=dev)
+        self.int_path = torch.zeros(self.N, dtype=torch.int32, device=dev)
         self.agg = torch.zeros(3, dtype=torch.float64, device=dev)
         self.cycles = None
         rc = self.lib.dragg_mpc_lds_bytes(ctypes.byref(self.dims))
@@ -185,7 +186,8 @@ class MPCBatch:
 
     def _out(self, hist=None):
         return L.Out(status=L.ptr(self.status), iters=L.ptr(self.iters), obj=L.ptr(self.obj),
-                     relax_obj=L.ptr(self.relax_obj), hist=L.ptr(hist), cycles=L.ptr(self.cycles))
+                     relax_obj=L.ptr(self.relax_obj), hist=L.ptr(hist), cycles=L.ptr(self.cycles),
+                     int_path=L.ptr(self.int_path))
 
     def enable_phase_timing(self, on=True):
         """Stamp per-phase shader cycles of every home into self.cycles [NPHASE][N] (diagnostic)."""

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DRAGG_MPC_ABI_VERSION 4
+#define DRAGG_MPC_ABI_VERSION 5
 
 /* home types (aggregator.py:425, 468, 520, 555); bit 0 = pv, bit 1 = battery */
 enum dragg_home_type {
@@ -152,6 +152,11 @@ typedef struct dragg_mpc_out {
     double* relax_obj;          /* [N] LP-relaxation objective (NaN if infeasible)     */
     double* hist;               /* optional [DRAGG_NVAL][N] copy of vals after the step */
     int64_t* cycles;            /* optional [DRAGG_NPHASE][N] shader cycles per phase   */
+    int32_t* int_path;          /* optional [N] integer-DP path (int_mode round): 0 = the
+                                   exact front DP solved both thermal chains; bit 0 / bit 1
+                                   = the indoor-air / tank chain used the bucketed
+                                   approximation (mixed-sign prices, a feasible set narrower
+                                   than one duty step, front overflow)                   */
 } dragg_mpc_out;
 
 /* solver phases timed into dragg_mpc_out.cycles (diagnostic; NULL = not stamped) */

@@ -228,7 +228,7 @@ def run(name, sc, hook=None):
     shutil.rmtree(work, ignore_errors=True)
     sys.path.remove(os.path.join(HERE, "refshim"))
     sys.path.remove(REF)
-    path = os.path.join(HERE, f"{name}.json.gz")
+    path = os.path.join(os.environ.get("GOLDEN_OUT_DIR", HERE), f"{name}.json.gz")
     with gzip.open(path, "wt") as f:
         json.dump(out, f, separators=(",", ":"))
     nst = {}

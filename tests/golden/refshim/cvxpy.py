@@ -218,6 +218,8 @@ class Minimize:
 class Problem:
     last_record = None
     time_limit = float(__import__("os").environ.get("GOLDEN_MILP_TIME_LIMIT", "60"))
+    # 0 = prove optimality outright (the proven-optimum fixtures); 1e-6 was round 1's setting
+    mip_rel_gap = float(__import__("os").environ.get("GOLDEN_MIP_REL_GAP", "1e-6"))
 
     def __init__(self, objective, constraints):
         self.objective = objective
@@ -275,7 +277,8 @@ class Problem:
             cons.append(LinearConstraint(A_ub, -np.inf, b_ub))
         return milp(cobj, constraints=cons, integrality=integ,
                     bounds=Bounds(-np.inf, np.inf),
-                    options={"time_limit": Problem.time_limit, "mip_rel_gap": 1e-6, "presolve": True})
+                    options={"time_limit": Problem.time_limit, "mip_rel_gap": Problem.mip_rel_gap,
+                             "presolve": True})
 
     def solve(self, solver=None, verbose=False, **kw):
         vars_, order, off, cobj, A_eq, b_eq, A_ub, b_ub, integ, c0 = self._assemble()
