@@ -2168,30 +2168,41 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         bh += tw(bh);
         if (k + 1 < H) { bl = fmax(bl, (double)B.flo[k + 1]); bh = fmin(bh, (double)B.fhi[k + 1]); }
         const double sl = dx > 0.0 ? bl : -bh, sh = dx > 0.0 ? bh : -bl;
-        // the children's key and cost ranges: the two bucket grids of this stage
+        // the children's key and cost ranges (widened past rounding): the two bucket grids of
+        // this stage.  A child's position in a range as a 32-bit fixed-point number
+        // v = (value - lo) * NTB * 2^23 / (hi - lo) gives its bucket (v >> 23) and, since v is
+        // computed to far better than one unit, conservative bounds v - 1 <= V <= v + 2 of
+        // the exact monotone position V: references use the bound that understates them,
+        // the tested child the one that overstates it.
         const double D = dx * g;
-        const double klo = fmax(sl, dx * fma(A, dx * smin, C) + fmin(0.0, D * SS));
-        const double khi = fmin(sh, dx * fma(A, dx * smax, C) + fmax(0.0, D * SS));
+        double klo = fmax(sl, dx * fma(A, dx * smin, C) + fmin(0.0, D * SS));
+        double khi = fmin(sh, dx * fma(A, dx * smax, C) + fmax(0.0, D * SS));
         if (!(klo <= khi)) return 0;                     // no child can stay feasible
-        const double clo = cmin + fmin(0.0, q * SS), chi = cmax + fmax(0.0, q * SS);
-        const double ikw = khi > klo ? (double)NTB / (khi - klo) : 0.0;
-        const double icw = chi > clo ? (double)NTB / (chi - clo) : 0.0;
-        auto kbucket = [&](double t) { return min(NTB - 1, max(0, (int)((t - klo) * ikw))); };
-        auto cbucket = [&](double c) { return min(NTB - 1, max(0, (int)((c - clo) * icw))); };
+        double clo = cmin + fmin(0.0, q * SS), chi = cmax + fmax(0.0, q * SS);
+        klo -= tw(klo); khi += tw(khi);
+        clo -= tw(clo); chi += tw(chi);
+        const double FX = (double)NTB * 8388608.0;      // NTB * 2^23 <= 2^31
+        const double ksc = FX / (khi - klo), csc = FX / (chi - clo);
+        double base[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) base[u] = fma(g, (double)u, C);
+        auto fixp = [](double y) { return y > 0.0 ? (unsigned)y : 0u; };   // y < 2^31 + 1
+        auto dn = [](unsigned v) { return v > 0u ? v - 1u : 0u; };
         // 1. per key bucket the cheapest child (largest key among equally cheap ones), per
-        //    cost bucket the largest key (cheapest among equal keys); bounds rounded outward
-        //    (cost up, key down) so that every reference is no better than a real child
+        //    cost bucket the largest-key child (cheapest among equal keys), both as
+        //    understated bounds (cost up, key down), by 64-bit LDS atomics
         for (int i = lane; i < n; i += WAVE) {
             const double2 Li = fa[i];
             const double xi = dx * Li.x;
 #pragma unroll
             for (int u = 0; u < NU; ++u) {
-                const double t = dx * fma(A, xi, fma(g, (double)u, C));
+                const double t = dx * fma(A, xi, base[u]);
                 if (t >= sl && t <= sh) {
                     const double c = fma(q, (double)u, Li.y);
-                    const unsigned cu = ord32(f32_up(c)), kd = ord32(f32_down(t));
-                    atomicMin(&B.kb[kbucket(t)], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
-                    atomicMax(&B.cb[cbucket(c)], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
+                    const unsigned vk = fixp((t - klo) * ksc), vc = fixp((c - clo) * csc);
+                    const unsigned cu = vc + 2u, kd = dn(vk);
+                    atomicMin(&B.kb[min(NTB - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
+                    atomicMax(&B.cb[min(NTB - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
                 }
             }
         }
@@ -2227,13 +2238,13 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         }
         __syncthreads();
         // 3. survivors appended to the other buffer in (parent, duty) order.  A child X is
-        //    dropped when some reference provably dominates it; X's own bounds are rounded
-        //    the other way (key up, cost down), so a dropped child is always dominated:
-        //    - a key bucket above holds a child no dearer:         cost_dn(X) >= mh
-        //    - its key bucket's cheapest child Y:   key_up(X) <= key(Y), cost_dn(X) >= cost(Y)
-        //    - a cost bucket below holds a child with no smaller key: key_up(X) <= kl
+        //    dropped when one of four references provably dominates it (X's bounds
+        //    overstated: key up, cost down):
+        //    - a key bucket above holds a child no dearer:          cost_dn(X) >= mh
+        //    - its key bucket's cheapest child Y:    key_up(X) <= key(Y), cost_dn(X) >= cost(Y)
+        //    - a cost bucket below holds a child with no smaller key:  key_up(X) <= kl
         //    - its cost bucket's largest-key child Y' likewise
-        //    (the two per-bucket tests need one strict inequality: X may be the reference)
+        //    (the per-bucket tests need one strict inequality: X may be the reference)
         int nn = 0;
         double nkmin = INFINITY, nkmax = -INFINITY, ncmin = INFINITY, ncmax = -INFINITY;
         for (int p = 0; p * WAVE < n; ++p) {
@@ -2243,12 +2254,13 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             const double xi = dx * Li.x;
 #pragma unroll
             for (int u = 0; u < NU; ++u) {
-                const double t = dx * fma(A, xi, fma(g, (double)u, C));
+                const double t = dx * fma(A, xi, base[u]);
                 const double c = fma(q, (double)u, Li.y);
                 bool keep = have && t >= sl && t <= sh;
                 if (keep) {
-                    const int kbk = kbucket(t), cbk = cbucket(c);
-                    const unsigned ku = ord32(f32_up(t)), cd = ord32(f32_down(c));
+                    const unsigned vk = fixp((t - klo) * ksc), vc = fixp((c - clo) * csc);
+                    const int kbk = min(NTB - 1, (int)(vk >> 23)), cbk = min(NTB - 1, (int)(vc >> 23));
+                    const unsigned ku = vk + 2u, cd = dn(vc);
                     const unsigned long long ky = B.kb[kbk], cy = B.cb[cbk];
                     const unsigned ycu = (unsigned)(ky >> 32), ykd = ~(unsigned)ky;
                     const unsigned zkd = (unsigned)(cy >> 32), zcu = ~(unsigned)cy;
