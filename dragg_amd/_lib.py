@@ -122,7 +122,9 @@ def ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
-def stream_ptr(stream=None):
+def stream_ptr(stream=None, device=None):
+    """The launch stream: `stream`, else the current stream of `device` (of the current device
+    when None)."""
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
+    s = stream if stream is not None else torch.cuda.current_stream(device)
     return ctypes.c_void_p(s.cuda_stream)

@@ -12,8 +12,9 @@ home on the host.  Here the community's state never leaves the GPU:
 * the per-step hash fields are appended to an on-device history (the
   `collected_data` lists), converted to the results.json layout only on request.
 
-Homes are sharded in contiguous blocks of the global community order; the season-noise
-stream is keyed by the GLOBAL home index, so results do not depend on the shard layout.
+Homes are sharded by stride (rank r solves global homes r, r + world, r + 2 world, ...: every
+shard carries the community's type mix); the season-noise stream is keyed by the GLOBAL home
+index, so results do not depend on the shard layout.
 """
 import numpy as np
 import torch

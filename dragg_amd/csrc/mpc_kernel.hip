@@ -2441,15 +2441,27 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
     return true;
 }
 
-template <bool EXPLICIT, int NT>
-__global__ __launch_bounds__(NT, 2) void mpc_direct_kernel(KArgs a) {   // 2 waves/SIMD: 8 homes per CU
+// The direct path is two launches over the same homes.  DM_FRONT (the hot one) runs the exact
+// front DP only; a home where it does not apply (mixed-sign prices, a too-narrow feasible
+// set, front overflow, S != 6) is flagged in the workspace and left untouched (nothing of
+// its hash written).  DM_BUCKET then solves exactly the flagged homes, each chain by the front
+// DP where it applies and by the bucketed DP otherwise.  Keeping the rarely needed bucketed DP
+// out of DM_FRONT keeps its register allocation out of the hot kernel.
+enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1 };
+
+template <bool EXPLICIT, int MODE>
+__global__ __launch_bounds__(WAVE, 2) void mpc_direct_kernel(KArgs a) {   // 2 waves/SIMD: 8 homes per CU
+    constexpr int NT = WAVE;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int home = blockIdx.x;
     const int lane = threadIdx.x;
     const int N = a.d.n_homes;
     if (home >= N) return;
-    Home h;
     const int H = a.d.horizon;
+    int* const defer = reinterpret_cast<int*>(reinterpret_cast<char*>(a.p.workspace) + par_region_bytes(N, H) +
+                                              (size_t)N * 8 * H * sizeof(double));
+    if (MODE == DM_BUCKET && defer[home] == 0) return;
+    Home h;
     LdsD D = carve_direct(smem, H, a.d.sub_steps);
     D.par = reinterpret_cast<uint16_t*>(a.p.workspace) + (size_t)home * H * NB_CAP;
     // the stage-slot solution lives in the workspace too (after every home's back-pointers):
@@ -2461,7 +2473,10 @@ __global__ __launch_bounds__(NT, 2) void mpc_direct_kernel(KArgs a) {   // 2 wav
     Prof pf;
     pf.start(a.out.cycles != nullptr);
     if (prologue<EXPLICIT>(a, h, L, io, lane, NT, D.sc) == DRAGG_ST_ERR_MISSING) {
-        if (lane == 0) write_missing(a, home);
+        if (lane == 0) {
+            write_missing(a, home);
+            defer[home] = 0;
+        }
         return;
     }
     derive(h);
@@ -2510,12 +2525,15 @@ __global__ __launch_bounds__(NT, 2) void mpc_direct_kernel(KArgs a) {   // 2 wav
             // the exact front DP; the bucketed DP only where it does not apply (mixed-sign
             // prices, a feasible set narrower than one duty step, front overflow, S != 6)
             int r = -1;
-            if (NT == WAVE && h.S == 6) {
+            if (h.S == 6) {
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par};
                 r = dp_front<6>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv);
             }
             if (r >= 0) {
                 ok = r == 1;
+            } else if (MODE == DM_FRONT) {                 // leave the home to DM_BUCKET
+                if (lane == 0) defer[home] = 1;
+                return;
             } else {
                 int_path |= 1 << chain;
                 ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
@@ -2548,6 +2566,7 @@ __global__ __launch_bounds__(NT, 2) void mpc_direct_kernel(KArgs a) {   // 2 wav
         a.out.obj[home] = obj;
         a.out.relax_obj[home] = NAN;
         if (a.out.int_path) a.out.int_path[home] = int_path;
+        if (MODE == DM_FRONT) defer[home] = 0;
     }
     if (a.out.hist && lane == 0)      // lane 0 wrote every vals field of this home
         for (int k = 0; k < DRAGG_NVAL; ++k) a.out.hist[(size_t)k * N + home] = io.v(k);
@@ -2562,8 +2581,7 @@ __global__ __launch_bounds__(256) void aggregate_kernel(const double* vals, int 
     const int keys[3] = {DRAGG_K_P_GRID, DRAGG_K_FORECAST_P_GRID, DRAGG_K_COST};
     for (int i = threadIdx.x; i < N; i += 256)
         for (int c = 0; c < 3; ++c) {
-            const double v = vals[(size_t)keys[c] * N + i];
-            if (v == v) s[c] += v;
+            s[c] += vals[(size_t)keys[c] * N + i];    // NaN (absent field) propagates
         }
     for (int c = 0; c < 3; ++c) red[c][threadIdx.x] = s[c];
     __syncthreads();
@@ -2589,7 +2607,10 @@ __global__ void noise_kernel(int N, int H, uint64_t seed, int off, int stride, i
 bool direct_mode(const dragg_mpc_dims* d) { return d->int_mode == DRAGG_INT_ROUND; }
 
 size_t workspace_bytes(const dragg_mpc_dims* d) {
-    return direct_mode(d) ? par_region_bytes(d->n_homes, d->horizon) + (size_t)d->n_homes * 8 * d->horizon * 8 : 0;
+    // [N][H][NB_CAP] u16 back-pointers, [N][8H] f64 solutions, [N] i32 DM_BUCKET flags
+    return direct_mode(d) ? par_region_bytes(d->n_homes, d->horizon) + (size_t)d->n_homes * 8 * d->horizon * 8 +
+                                (size_t)d->n_homes * sizeof(int)
+                          : 0;
 }
 
 size_t kernel_lds_bytes(const dragg_mpc_dims* d) {
@@ -2603,17 +2624,6 @@ int check_dims(const dragg_mpc_dims* d) {
     if (direct_mode(d) && !direct_fits(d->horizon)) return DRAGG_E_HORIZON;
     if (kernel_lds_bytes(d) > 160 * 1024) return DRAGG_E_HORIZON;
     return DRAGG_OK;
-}
-
-// threads per home of the direct kernel (64, 128 or 256); DRAGG_DIRECT_THREADS overrides
-int direct_threads() {
-    static int nt = 0;
-    if (nt == 0) {
-        const char* e = getenv("DRAGG_DIRECT_THREADS");
-        const int v = e ? atoi(e) : 0;
-        nt = (v == 128 || v == 256) ? v : 64;
-    }
-    return nt;
 }
 
 template <typename K>
@@ -2633,11 +2643,9 @@ template <bool EXPLICIT>
 int launch(const KArgs& a, hipStream_t s) {
     static int attr[4] = {0, 0, 0, 0};
     if (!direct_mode(&a.d)) return launch_kernel(mpc_home_kernel<EXPLICIT>, attr[0], a, 64, s);
-    switch (direct_threads()) {
-        case 128: return launch_kernel(mpc_direct_kernel<EXPLICIT, 128>, attr[2], a, 128, s);
-        case 256: return launch_kernel(mpc_direct_kernel<EXPLICIT, 256>, attr[3], a, 256, s);
-        default: return launch_kernel(mpc_direct_kernel<EXPLICIT, 64>, attr[1], a, 64, s);
-    }
+    const int rc = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT>, attr[1], a, WAVE, s);
+    if (rc) return rc;
+    return launch_kernel(mpc_direct_kernel<EXPLICIT, DM_BUCKET>, attr[2], a, WAVE, s);
 }
 
 }  // namespace

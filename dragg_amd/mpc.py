@@ -111,6 +111,8 @@ class MPCBatch:
         if not torch.cuda.is_available():
             raise L.DraggError("no GPU visible: the batched MPC has no CPU fallback")
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.homes = homes
         self.names = [h["name"] for h in homes]
         P, types, draws, dm = pack_homes(homes, template_home)
@@ -196,17 +198,25 @@ class MPCBatch:
     # ------------------------------------------------------------------ launches
     def step(self, t, noise=None, hist=None, stream=None):
         """One closed-loop timestep for every home (run_iteration, aggregator.py:711-726)."""
+        with torch.cuda.device(self.device):
+            return self._step(t, noise, hist, stream)
+
+    def _step(self, t, noise, hist, stream):
         if noise is not None:
             noise = noise.to(device=self.device, dtype=torch.float64).contiguous()
             assert tuple(noise.shape) == (self.H, self.N)
         prob, hsh, out = self._problem(), self._hash(), self._out(hist)
         L.check(self.lib.dragg_mpc_step(ctypes.byref(self.dims), ctypes.byref(prob), ctypes.byref(hsh),
-                                        ctypes.byref(out), int(t), L.ptr(noise), L.stream_ptr(stream)))
+                                        ctypes.byref(out), int(t), L.ptr(noise), L.stream_ptr(stream, self.device)))
         self._keep = (noise, hist)
         return self.status
 
     def solve_explicit(self, t, T0, Tw0, E0, counter, winter, draw, oat, ghi, price, stream=None):
         """Independent per-home solves with explicit inputs ([N] and [H+1 or H][N] arrays)."""
+        with torch.cuda.device(self.device):
+            return self._solve_explicit(t, T0, Tw0, E0, counter, winter, draw, oat, ghi, price, stream)
+
+    def _solve_explicit(self, t, T0, Tw0, E0, counter, winter, draw, oat, ghi, price, stream):
         dev, N, H = self.device, self.N, self.H
 
         def d(x, shape, dtype=torch.float64):
@@ -222,22 +232,33 @@ class MPCBatch:
         ex = L.Explicit(**{k: L.ptr(v) for k, v in ex_t.items()})
         prob, hsh, out = self._problem(), self._hash(), self._out()
         L.check(self.lib.dragg_mpc_solve_explicit(ctypes.byref(self.dims), ctypes.byref(prob), ctypes.byref(ex),
-                                                  ctypes.byref(hsh), ctypes.byref(out), L.stream_ptr(stream)))
+                                                  ctypes.byref(hsh), ctypes.byref(out),
+                                                  L.stream_ptr(stream, self.device)))
         self._keep = ex_t
         return self.status
 
     def aggregate(self, stream=None):
-        """collect_data sums (aggregator.py:751-753) -> device tensor [agg_load, forecast_load, agg_cost]."""
+        """collect_data sums (aggregator.py:751-753) -> device tensor [agg_load, forecast_load, agg_cost].
+        A home whose fields are absent (a crashed home: the reference raises KeyError in
+        collect_data, aggregator.py:750-752) makes the sums NaN."""
+        with torch.cuda.device(self.device):
+            return self._aggregate(stream)
+
+    def _aggregate(self, stream):
         hsh = self._hash()
         L.check(self.lib.dragg_mpc_aggregate(ctypes.byref(self.dims), ctypes.byref(hsh), L.ptr(self.agg),
-                                             L.stream_ptr(stream)))
+                                             L.stream_ptr(stream, self.device)))
         return self.agg
 
     def season_noise(self, t, stream=None):
+        with torch.cuda.device(self.device):
+            return self._season_noise(t, stream)
+
+    def _season_noise(self, t, stream):
         out = torch.empty((self.H, self.N), dtype=torch.float64, device=self.device)
         L.check(self.lib.dragg_mpc_season_noise(ctypes.byref(self.dims), self.seed, self.home_offset,
                                                 self.home_stride, int(t), L.ptr(out),
-                                                L.stream_ptr(stream)))
+                                                L.stream_ptr(stream, self.device)))
         return out
 
     # ------------------------------------------------------------------ hash views

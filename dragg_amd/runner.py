@@ -116,6 +116,10 @@ class Aggregator:
             self.dev.collect_data(defer=True)      # no feedback: the sums are reduced at the end
             self.timestep = t + 1
             if (t + 1) % self.checkpoint_interval == 0:
+                # the reference raises inside the step that fails (mpc_calc.py:280-289,
+                # 537-539); checking at each checkpoint (one host sync) keeps post-error data
+                # out of every results.json written
+                self.dev.check_errors()
                 self.write_outputs()
         self.dev.reduce_history()
         self.dev.check_errors()
@@ -229,6 +233,10 @@ class Aggregator:
         for t in range(self.num_timesteps):
             self.rl_step(policy(self))
             if (t + 1) % self.checkpoint_interval == 0:
+                # the reference raises inside the step that fails (mpc_calc.py:280-289,
+                # 537-539); checking at each checkpoint (one host sync) keeps post-error data
+                # out of every results.json written
+                self.dev.check_errors()
                 self.write_outputs()
         self.dev.check_errors()
         return self.write_outputs()

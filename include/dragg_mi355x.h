@@ -211,7 +211,8 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
                              dragg_mpc_out* out, void* stream);
 
 /* collect_data sums (aggregator.py:751-753): out3 = {sum p_grid_opt, sum
-   forecast_p_grid_opt, sum cost_opt} over homes whose fields are present. */
+   forecast_p_grid_opt, sum cost_opt} over the shard's homes; an absent field (NaN: a home
+   the reference would have crashed on, KeyError at aggregator.py:750-752) makes its sum NaN. */
 int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, double* out3,
                         void* stream);
 

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Exact thermal optima of every golden-fixture solve -- TEST INFRASTRUCTURE (this container).
+
+For every record of tests/golden/*.json.gz and tests/golden/proven/*.json.gz, solves the
+reference's thermal integer programme with oracle/thermal.py (assumption-free backward
+step-function DP, itself pinned by tests/test_oracle_thermal.py against enumeration and HiGHS)
+and writes tests/golden/proven/thermal_exact.json.gz: per scenario and record the exact
+indoor-air and tank chain costs (None where a chain has no integer schedule), plus whether the
+record's duty prices have one sign (where the GPU's Pareto-front DP applies).  The GPU test
+tests/test_gpu_exact.py compares the kernel's integer solutions with these numbers, so the GPU
+box needs neither the oracle run nor scipy.
+
+Usage:  python tests/golden/make_thermal_exact.py
+"""
+import glob
+import gzip
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import mpc as M          # noqa: E402
+from oracle import thermal as TH     # noqa: E402
+
+
+def si_of(r):
+    return M.StepInput(t=r["t"], T0=r["T0"], Tw0=r["Tw0"], E0=r["E0"], oat=np.array(r["oat"]),
+                       ghi=np.array(r["ghi"]), price=np.array(r["total_price"]), draw=np.array(r["draw_size"]),
+                       winter=r["season"] == "winter")
+
+
+def main():
+    files = sorted(glob.glob(os.path.join(HERE, "*.json.gz"))) + sorted(glob.glob(os.path.join(HERE, "proven", "h48_*.json.gz")))
+    out = {}
+    for path in files:
+        with gzip.open(path, "rt") as f:
+            d = json.load(f)
+        name = os.path.basename(path)[:-8]
+        if path.startswith(os.path.join(HERE, "proven")):
+            name = "proven/" + name
+        homes = {h["name"]: h for h in d["homes"]}
+        rows = []
+        for r in d["records"]:
+            hc = M.home_const(homes[r["name"]])
+            si = si_of(r)
+            chT = TH.chain_T(hc, si)
+            uniform = bool(np.all(chT["q"] >= 0) or np.all(chT["q"] <= 0))
+            T = TH.solve_chain(chT)
+            W = TH.solve_chain(TH.chain_W(hc, si, T[2])) if T is not None else None
+            rows.append(dict(uniform=uniform, cost_T=None if T is None else T[0], cost_W=None if W is None else W[0]))
+        out[name] = rows
+        n_ok = sum(1 for x in rows if x["cost_W"] is not None)
+        print(f"{name}: {len(rows)} records, {n_ok} with an integer schedule", flush=True)
+    path = os.path.join(HERE, "proven", "thermal_exact.json.gz")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with gzip.open(path, "wt") as f:
+        json.dump(out, f, separators=(",", ":"))
+    print(path, os.path.getsize(path))
+
+
+if __name__ == "__main__":
+    main()

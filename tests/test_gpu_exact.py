@@ -1,0 +1,97 @@
+"""GPU integer DP == the exact thermal optimum, record by record (int_mode round, the default).
+
+The reference's MILP (`mpc_calc.py:291-451`) is the thermal integer programme plus the battery
+and PV LPs (separable).  tests/golden/proven/thermal_exact.json.gz holds, for
+every solve of every golden fixture, the exact optimum of the two thermal chains computed by
+oracle/thermal.py (an assumption-free backward step-function DP, pinned against enumeration and
+HiGHS by tests/test_oracle_thermal.py).  Here the kernel's integer schedules, read back from the
+hash fields it writes, must cost exactly that (1e-9 relative) on every record whose prices have
+one sign -- where the kernel's exact Pareto-front DP applies and must not fall back -- and the
+status (integer schedule or none) must agree.  Mixed-sign records (RL reward prices) run the
+bucketed fallback: their gap is reported, and bounded.
+"""
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests import fixtures as F
+
+pytestmark = pytest.mark.gpu
+
+EXACT = os.path.join(F.GOLDEN, "proven", "thermal_exact.json.gz")
+
+
+def _exact():
+    with gzip.open(EXACT, "rt") as f:
+        return json.load(f)
+
+
+def _solve(d):
+    import torch
+    from dragg_amd import _lib as L
+    from dragg_amd.mpc import MPCBatch
+    recs = d["records"]
+    homes, ex = F.explicit_inputs(d, recs)
+    b = MPCBatch(homes, int_mode="round")
+    fc, vals = F.prev_hash_arrays(recs, b.H, L.FC_KEYS, L.VAL_KEYS)
+    b.fc.copy_(torch.tensor(fc))
+    b.vals.copy_(torch.tensor(vals))
+    b.solve_explicit(**ex)
+    torch.cuda.synchronize()
+    return dict(status=b.status.cpu().numpy(), fc=b.fc.cpu().numpy(), path=b.int_path.cpu().numpy(), S=b.S)
+
+
+def _thermal_cost(r, fc, i, S):
+    """sum_k q_k u_k of the kernel's duties (hash fields are duty / S, mpc_calc.py:503-505)."""
+    from dragg_amd import _lib as L
+    H = fc.shape[1]
+    w = 0.92 ** np.arange(H) * np.asarray(r["total_price"][:H], float)
+    key = "hvac_heat_on_opt" if r["season"] == "winter" else "hvac_cool_on_opt"
+    u = np.rint(fc[L.FC_KEYS.index(key), :, i] * S)
+    wh = np.rint(fc[L.FC_KEYS.index("wh_heat_on_opt"), :, i] * S)
+    return u, wh, w
+
+
+@pytest.mark.parametrize("name", F.scenarios())
+def test_integer_dp_is_exact(name, gpu):
+    from dragg_amd import _lib as L
+    from oracle import mpc as M
+    d = F.load(name)
+    ex = _exact()[name]
+    res = _solve(d)
+    homes = {h["name"]: h for h in d["homes"]}
+    n_exact = n_fallback = 0
+    gaps = []
+    for i, r in enumerate(d["records"]):
+        e = ex[i]
+        st = res["status"][i]
+        if st not in (L.ST_OPTIMAL, L.ST_ROUND_FAIL):
+            continue                     # decided before the DP (presolve infeasible, fallback)
+        has = e["cost_W"] is not None
+        assert (st == L.ST_OPTIMAL) == has, (name, i, r["name"], r["t"], L.STATUS_NAMES[st], e)
+        if not has:
+            continue
+        hc = M.home_const(homes[r["name"]])
+        u, wh, w = _thermal_cost(r, res["fc"], i, res["S"])
+        P = hc.Ph if r["season"] == "winter" else hc.Pc
+        ours = float(w @ (u * (hc.S * P)) + w @ (wh * (hc.S * hc.Pw)))
+        ref = e["cost_T"] + e["cost_W"]
+        gap = (ours - ref) / max(1.0, abs(ref))
+        if e["uniform"]:
+            assert res["path"][i] == 0, (name, i, "exact DP fell back", res["path"][i])
+            assert abs(gap) <= 1e-9, (name, i, r["name"], r["t"], ours, ref)
+            n_exact += 1
+        else:
+            n_fallback += 1
+            gaps.append(gap)
+            assert gap >= -1e-9, (name, i, ours, ref)      # never below the exact optimum
+    gaps = np.array(gaps)
+    msg = f"{name}: {n_exact} records exact (gap <= 1e-9)"
+    if len(gaps):
+        msg += f"; {n_fallback} mixed-sign records on the bucketed fallback: gap max {gaps.max():.2e}, " \
+               f"{int((gaps > 1e-9).sum())} above 1e-9"
+        assert gaps.max() <= 0.01
+    print(msg)

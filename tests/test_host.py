@@ -151,9 +151,15 @@ def test_size_queries_without_gpu(lib_path):
     d = L.Dims(n_homes=100, horizon=24, sub_steps=6, dt=4, n_draw_hours=48, n_env=0, n_rp=1,
                int_mode=L.INT_ROUND, max_iter=0, check_every=0, discount=0.92)
     ws = lib.dragg_mpc_workspace_bytes(ctypes.byref(d))
-    assert ws % (100 * 24 * 2) == 0 and ws // (100 * 24 * 2) >= 330   # uint16 per bucket and stage
+    # u16 back-pointer per front label and stage (NB_CAP = 336), rounded to 256 B, then the
+    # [N][8H] f64 stage-slot solutions and the [N] i32 flags of the bucketed second launch
+    par = (100 * 24 * 336 * 2 + 255) // 256 * 256
+    assert ws == par + 100 * 8 * 24 * 8 + 100 * 4
     lds_direct = lib.dragg_mpc_lds_bytes(ctypes.byref(d))
     assert 0 < lds_direct <= 20 * 1024                 # 8 homes per CU at H = 24
+    d.horizon = 48
+    assert 0 < lib.dragg_mpc_lds_bytes(ctypes.byref(d)) <= 20 * 1024   # and at H = 48
+    d.horizon = 24
     d.int_mode = L.INT_RELAX
     assert lib.dragg_mpc_workspace_bytes(ctypes.byref(d)) == 0
     assert lib.dragg_mpc_lds_bytes(ctypes.byref(d)) > lds_direct

@@ -1,0 +1,71 @@
+"""The exact thermal-chain checker (oracle/thermal.py) against enumeration and HiGHS.
+
+CPU only.  The checker is what the GPU's integer DP is held to (tests/test_gpu_exact.py), so it
+is pinned here first: (1) on random tiny chains it equals a brute-force enumeration of every
+duty schedule, for either sign of the prices; (2) on the reference's own solves it reproduces
+the MILP optimum of every base home (no battery, no PV: the MILP is the thermal part alone)
+that HiGHS proved optimal, and is never worse than a HiGHS incumbent.  (The fixtures' MILP
+objectives are c.x of HiGHS's own solution, whose continuous columns carry its ~1e-7 feasibility
+slack: the comparison bound is 2e-6 relative.)
+"""
+import numpy as np
+import pytest
+
+from oracle import mpc as M
+from oracle import thermal as TH
+from tests import fixtures as F
+
+
+def _random_chain(rng, H, S, sign):
+    A = rng.uniform(0.6, 1.0, H)
+    g = rng.choice([-1.0, 1.0]) * rng.uniform(0.2, 0.6)
+    C = rng.normal(0, 0.3, H)
+    q = rng.uniform(0.05, 1.0, H) * (1 if sign == "pos" else -1 if sign == "neg" else rng.choice([-1, 1], H))
+    return dict(A=A, C=C, q=q, g=g, x0=rng.uniform(-0.5, 0.5), lo0=-1.0 - rng.uniform(0, 0.3), hi0=1.0,
+                lo=-1.0, hi=1.0 + rng.uniform(0, 0.3), S=S)
+
+
+@pytest.mark.parametrize("sign", ["pos", "neg", "mixed"])
+def test_exact_chain_equals_enumeration(sign):
+    rng = np.random.default_rng({"pos": 1, "neg": 2, "mixed": 3}[sign])
+    n_feas = 0
+    for _ in range(60):
+        ch = _random_chain(rng, H=5, S=3, sign=sign)
+        bf = TH.brute_force(ch)
+        ex = TH.solve_chain(ch)
+        if bf is None:
+            assert ex is None
+            continue
+        n_feas += 1
+        assert ex is not None
+        assert abs(ex[0] - bf) <= 1e-12 * max(1.0, abs(bf)), (ex[0], bf)
+        assert abs(float(np.dot(ch["q"], ex[1])) - ex[0]) <= 1e-12 * max(1.0, abs(bf))
+    assert n_feas >= 20
+
+
+def _si(r):
+    return M.StepInput(t=r["t"], T0=r["T0"], Tw0=r["Tw0"], E0=r["E0"], oat=np.array(r["oat"]),
+                       ghi=np.array(r["ghi"]), price=np.array(r["total_price"]), draw=np.array(r["draw_size"]),
+                       winter=r["season"] == "winter")
+
+
+@pytest.mark.parametrize("name", ["c1_h24", "spring_dt1", "summer_dt1"])
+def test_exact_thermal_matches_reference_milp_on_base_homes(name):
+    d = F.load(name)
+    homes = {h["name"]: h for h in d["homes"]}
+    n_proven = n_incumbent = 0
+    for r in d["records"][::2]:
+        if r["status"] != "optimal" or r["type"] != "base" or r["milp_obj"] is None:
+            continue
+        hc = M.home_const(homes[r["name"]])
+        th = TH.thermal_optimum(hc, _si(r))
+        assert th is not None, (name, r["name"], r["t"])
+        ref = r["milp_obj"]
+        if r["milp_status"] == 0:        # proven (HiGHS, mip_rel_gap <= 1e-6)
+            n_proven += 1
+            assert abs(th["cost"] - ref) <= 2e-6 * max(1.0, abs(ref)), (name, r["name"], r["t"], th["cost"], ref)
+        else:                            # a time-limited incumbent: the exact optimum is no worse
+            n_incumbent += 1
+            assert th["cost"] <= ref + 2e-6 * max(1.0, abs(ref)), (name, r["name"], r["t"], th["cost"], ref)
+    assert n_proven >= 5
+    print(f"{name}: {n_proven} proven base-home optima reproduced, {n_incumbent} incumbents not beaten")
