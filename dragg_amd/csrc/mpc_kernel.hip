@@ -2153,12 +2153,13 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         if (empty) return 0;
         if (narrow) return -1;
     }
+    // the front stores each label's exact STATE x (not its key dx * x) and cost
     double2* fa = B.fa;
     double2* fb = B.fb;
-    if (lane == 0) fa[0] = make_double2(dx * x0, 0.0);
+    if (lane == 0) fa[0] = make_double2(x0, 0.0);
     int n = 1;
-    double smin = dx * x0, smax = dx * x0, cmin = 0.0, cmax = 0.0;   // key / cost range of the front
-    const unsigned long long below = (1ull << lane) - 1ull;          // lanes < this one
+    double xmin = x0, xmax = x0, cmin = 0.0, cmax = 0.0;    // state / cost range of the front
+    const unsigned long long below = (1ull << lane) - 1ull;  // lanes < this one
     for (int b = lane; b < NTB; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
     __syncthreads();
     for (int k = 0; k < H; ++k) {
@@ -2167,39 +2168,39 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         bl -= tw(bl);
         bh += tw(bh);
         if (k + 1 < H) { bl = fmax(bl, (double)B.flo[k + 1]); bh = fmin(bh, (double)B.fhi[k + 1]); }
-        const double sl = dx > 0.0 ? bl : -bh, sh = dx > 0.0 ? bh : -bl;
-        // the children's key and cost ranges (widened past rounding): the two bucket grids of
-        // this stage.  A child's position in a range as a 32-bit fixed-point number
-        // v = (value - lo) * NTB * 2^23 / (hi - lo) gives its bucket (v >> 23) and, since v is
-        // computed to far better than one unit, conservative bounds v - 1 <= V <= v + 2 of
-        // the exact monotone position V: references use the bound that understates them,
-        // the tested child the one that overstates it.
-        const double D = dx * g;
-        double klo = fmax(sl, dx * fma(A, dx * smin, C) + fmin(0.0, D * SS));
-        double khi = fmin(sh, dx * fma(A, dx * smax, C) + fmax(0.0, D * SS));
-        if (!(klo <= khi)) return 0;                     // no child can stay feasible
+        // the children's state and cost ranges (widened past rounding) define the two bucket
+        // grids of this stage.  A child's position in a range as a 32-bit fixed-point number
+        // v = (key - lo) * NTB * 2^23 / (hi - lo) (one fma from the state) gives its bucket
+        // (v >> 23) and, v being computed to far better than one unit, conservative bounds
+        // v - 1 <= V <= v + 2 of the exact monotone position V: references use the bound that
+        // understates them, the tested child the one that overstates it.
+        double xl = fmax(bl, fma(A, xmin, C) + fmin(0.0, g * SS));
+        double xh = fmin(bh, fma(A, xmax, C) + fmax(0.0, g * SS));
+        if (!(xl <= xh)) return 0;                       // no child can stay feasible
+        xl -= tw(xl); xh += tw(xh);
         double clo = cmin + fmin(0.0, q * SS), chi = cmax + fmax(0.0, q * SS);
-        klo -= tw(klo); khi += tw(khi);
         clo -= tw(clo); chi += tw(chi);
-        const double FX = (double)NTB * 8388608.0;      // NTB * 2^23 <= 2^31
-        const double ksc = FX / (khi - klo), csc = FX / (chi - clo);
+        const double FX = (double)NTB * 8388608.0;        // NTB * 2^23 <= 2^31
+        const double ksc = FX / (xh - xl), csc = FX / (chi - clo);
+        // key position: (dx x - key_lo) * ksc with key_lo = dx > 0 ? xl : -xh
+        const double kmul = dx * ksc, kadd = -(dx > 0.0 ? xl : -xh) * ksc;
+        const double cadd = -clo * csc;
         double base[NU];
 #pragma unroll
         for (int u = 0; u < NU; ++u) base[u] = fma(g, (double)u, C);
-        auto fixp = [](double y) { return y > 0.0 ? (unsigned)y : 0u; };   // y < 2^31 + 1
-        auto dn = [](unsigned v) { return v > 0u ? v - 1u : 0u; };
+        auto fixp = [](double y) { return (unsigned)fmax(y, 0.0); };   // y < 2^31 + 1
+        auto dn = [](unsigned v) { return max(v, 1u) - 1u; };
         // 1. per key bucket the cheapest child (largest key among equally cheap ones), per
         //    cost bucket the largest-key child (cheapest among equal keys), both as
         //    understated bounds (cost up, key down), by 64-bit LDS atomics
         for (int i = lane; i < n; i += WAVE) {
             const double2 Li = fa[i];
-            const double xi = dx * Li.x;
 #pragma unroll
             for (int u = 0; u < NU; ++u) {
-                const double t = dx * fma(A, xi, base[u]);
-                if (t >= sl && t <= sh) {
+                const double xc = fma(A, Li.x, base[u]);
+                if (xc >= bl && xc <= bh) {
                     const double c = fma(q, (double)u, Li.y);
-                    const unsigned vk = fixp((t - klo) * ksc), vc = fixp((c - clo) * csc);
+                    const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(c, csc, cadd));
                     const unsigned cu = vc + 2u, kd = dn(vk);
                     atomicMin(&B.kb[min(NTB - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
                     atomicMax(&B.cb[min(NTB - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
@@ -2246,19 +2247,18 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         //    - its cost bucket's largest-key child Y' likewise
         //    (the per-bucket tests need one strict inequality: X may be the reference)
         int nn = 0;
-        double nkmin = INFINITY, nkmax = -INFINITY, ncmin = INFINITY, ncmax = -INFINITY;
+        double nxmin = INFINITY, nxmax = -INFINITY, ncmin = INFINITY, ncmax = -INFINITY;
         for (int p = 0; p * WAVE < n; ++p) {
             const int i = lane + p * WAVE;
             const bool have = i < n;
             const double2 Li = have ? fa[i] : make_double2(0.0, 0.0);
-            const double xi = dx * Li.x;
 #pragma unroll
             for (int u = 0; u < NU; ++u) {
-                const double t = dx * fma(A, xi, base[u]);
+                const double xc = fma(A, Li.x, base[u]);
                 const double c = fma(q, (double)u, Li.y);
-                bool keep = have && t >= sl && t <= sh;
+                bool keep = have && xc >= bl && xc <= bh;
                 if (keep) {
-                    const unsigned vk = fixp((t - klo) * ksc), vc = fixp((c - clo) * csc);
+                    const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(c, csc, cadd));
                     const int kbk = min(NTB - 1, (int)(vk >> 23)), cbk = min(NTB - 1, (int)(vc >> 23));
                     const unsigned ku = vk + 2u, cd = dn(vc);
                     const unsigned long long ky = B.kb[kbk], cy = B.cb[cbk];
@@ -2274,10 +2274,10 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
                 const int slot = nn + __popcll(bal & below);
                 nn += __popcll(bal);
                 if (keep && slot < NF) {
-                    fb[slot] = make_double2(t, c);
+                    fb[slot] = make_double2(xc, c);
                     B.par[k * NB_CAP + slot] = (uint16_t)(i | (u << 12));
-                    nkmin = fmin(nkmin, t);
-                    nkmax = fmax(nkmax, t);
+                    nxmin = fmin(nxmin, xc);
+                    nxmax = fmax(nxmax, xc);
                     ncmin = fmin(ncmin, c);
                     ncmax = fmax(ncmax, c);
                 }
@@ -2285,8 +2285,8 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         }
         if (nn == 0) return 0;                       // no child left inside the feasible set
         if (nn > NF) return -1;                      // front overflow
-        smin = dpp_reduce(nkmin, [](double a, double b) { return fmin(a, b); });
-        smax = dpp_reduce(nkmax, [](double a, double b) { return fmax(a, b); });
+        xmin = dpp_reduce(nxmin, [](double a, double b) { return fmin(a, b); });
+        xmax = dpp_reduce(nxmax, [](double a, double b) { return fmax(a, b); });
         cmin = dpp_reduce(ncmin, [](double a, double b) { return fmin(a, b); });
         cmax = dpp_reduce(ncmax, [](double a, double b) { return fmax(a, b); });
         for (int b = lane; b < NTB; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
