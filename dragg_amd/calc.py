@@ -16,13 +16,34 @@ from . import _lib as L
 from .inputs import max_load
 from .mpc import MPCBatch
 
+# The reference's plug point: home['hems']['solver'] names a cvxpy MILP backend, and an
+# unknown name falls back to GLPK_MI (mpc_calc.py:141-145).  Every one of them solves the same
+# MILP to optimality, so every one maps to this build's exact MILP path (int_mode "round");
+# the build's own modes may be named directly ("relax": the LP relaxation, "round_lp").
+SOLVER_MODES = {"GLPK_MI": "round", "GUROBI": "round", "ECOS": "round"}
+
+
+def int_mode_for(home):
+    """The int_mode a home's hems.solver selects (mpc_calc.py:141-145)."""
+    name = str(home.get("hems", {}).get("solver", "GLPK_MI"))
+    if name in L.INT_MODES:
+        return name
+    return SOLVER_MODES.get(name, "round")
+
 
 class Community:
     """The redis side of a run for a set of homes: environment lists, `current_values`
-    timestep, `reward_price`, and the per-home hashes (device resident)."""
+    timestep, `reward_price`, and the per-home hashes (device resident).
 
-    def __init__(self, homes, oat, ghi, tou, start_hour_index, reward_price=(0.0,), int_mode="round", seed=0,
+    The reference's MPCCalc(home) reads its environment from the redis server the aggregator
+    filled (mpc_calc.py:117-132); here `make_default()` plays that role: MPCCalc(home) without a
+    community attaches to the default one."""
+
+    _default = None
+
+    def __init__(self, homes, oat, ghi, tou, start_hour_index, reward_price=(0.0,), int_mode=None, seed=0,
                  device="cuda"):
+        int_mode = int_mode or (int_mode_for(homes[0]) if homes else "round")
         self.batch = MPCBatch(homes, oat, ghi, tou, start_hour_index, reward_price, int_mode=int_mode, seed=seed,
                               device=device)
         self.index = {h["name"]: i for i, h in enumerate(homes)}
@@ -48,6 +69,18 @@ class Community:
     def hgetall(self, name):
         return self.batch.hash_dict(self.index[name], as_str=True)
 
+    def make_default(self):
+        """Register as the community that MPCCalc(home) attaches to."""
+        Community._default = self
+        return self
+
+    @classmethod
+    def default(cls):
+        if cls._default is None:
+            raise RuntimeError("no community: build one with Community(...).make_default() first (the reference "
+                               "needs its redis server filled by the aggregator, mpc_calc.py:117-132)")
+        return cls._default
+
 
 def manage_home(home):
     """mpc_calc.py:16-22."""
@@ -55,7 +88,17 @@ def manage_home(home):
 
 
 class MPCCalc:
-    def __init__(self, home, community):
+    """mpc_calc.py:24-98: `MPCCalc(home)` (the default community) or `MPCCalc(home, community)`."""
+
+    def __init__(self, home, community=None):
+        community = community if community is not None else Community.default()
+        if home["name"] not in community.index:
+            raise KeyError(f"home {home['name']!r} is not part of the community")
+        want = int_mode_for(home)
+        have = [k for k, v in L.INT_MODES.items() if v == community.batch.dims.int_mode][0]
+        if want != have:
+            raise ValueError(f"home {home['name']!r} asks for solver {home['hems'].get('solver')!r} "
+                             f"(int_mode {want!r}) but its community solves with {have!r}")
         self.home = home
         self.name = home["name"]
         self.type = home["type"]

@@ -25,6 +25,10 @@ constexpr int NS = 8;        // variable slots per stage
 constexpr int NR = 3;        // dynamics rows per stage
 constexpr int RS = 4;        // row stride per stage in LDS
 constexpr int WAVE = 64;
+constexpr int NB_CAP = 336;          // DP buckets per chain (config ranges need <= ~327 at any dt)
+constexpr int NBND = 8;              // box-boundary buckets per stage (dp_zspace; 4-5 in practice)
+constexpr int NF = NB_CAP;          // exact front DP: labels per stage (dp_front)
+constexpr int NTB = 256;             // key buckets and cost buckets per stage (dp_front)
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
 
 constexpr double SIGMA = 1e-6;
@@ -1006,27 +1010,15 @@ DEV bool dp_chain(const Home& h, const Lds& L, const DpChain& c, int lane) {
     return true;
 }
 
-DEV bool round_duties(const Home& h, const Lds& L, int lane) {
-    const int H = h.H;
-    // coefficient arrays live in L.yeq / L.zeq (4H each, free after the ADMM)
-    double* cA = L.yeq;
-    double* cC = L.zeq;
-    for (int k = lane; k < H; k += WAVE) {
-        cA[k] = h.aT;
-        cC[k] = L.oat[k + 1] * h.iR * 3600 * h.inv_c;
-    }
-    __syncthreads();
-    DpChain cT{H, h.S, S_T, S_U, h.g, cA, cC, h.T0};
-    if (!dp_chain(h, L, cT, lane)) return false;
-    for (int k = lane; k < H; k += WAVE) {
-        const double df = L.draw[k + 1] / h.V, rem = 1 - df, d15 = df * TAP;
-        cA[k] = rem + (-rem * h.iRw) * 3600 * h.inv_w;
-        cC[k] = h.e * L.x[k * 8 + S_T] + (d15 + ((-d15) * h.iRw) * 3600 * h.inv_w);
-    }
-    __syncthreads();
-    DpChain cW{H, h.S, S_TW, S_W, h.f, cA, cC, h.Tw0};
-    return dp_chain(h, L, cW, lane);
-}
+template <int SS>
+DEV int dp_front(const struct FrontBufs& B, int H, int lane, double g, double x0, double lo0, double hi0, double lo,
+                 double hi, int sx, int sv);
+
+// int_mode round_lp: the integer duties after the relaxation, by the exact front DP (the
+// default path's, dp_front) with its buffers in the KKT-factor LDS the ADMM no longer needs
+// and its back-pointers in the workspace; the binned dp_chain only where the front DP does not
+// apply (mixed-sign prices, a too-narrow feasible set, S != 6)
+DEV bool round_duties(const Home& h, const Lds& L, int lane, uint16_t* par);
 
 // closed-form PV curtailment (mpc_calc.py:382-384): u multiplies a cost coefficient
 // gamma^k price_k S A eta ghi_k / 1000, so u = 1 only where that coefficient is negative
@@ -1317,7 +1309,10 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
     if (status == DRAGG_ST_OPTIMAL) {
         relax = objective(h, L, lane);
         pf.mark(DRAGG_PH_WRITE);
-        if (a.d.int_mode == DRAGG_INT_ROUND_LP && !round_duties(h, L, lane)) status = DRAGG_ST_ROUND_FAIL;
+        if (a.d.int_mode == DRAGG_INT_ROUND_LP &&
+            !round_duties(h, L, lane, a.p.workspace ? reinterpret_cast<uint16_t*>(a.p.workspace) +
+                                                          (size_t)home * H * NB_CAP : nullptr))
+            status = DRAGG_ST_ROUND_FAIL;
         pf.mark(DRAGG_PH_INTEGER);
         if (status == DRAGG_ST_OPTIMAL) obj = objective(h, L, lane);
     }
@@ -1356,11 +1351,6 @@ __global__ __launch_bounds__(64) void mpc_home_kernel(KArgs a) {
 // No relaxation / ADMM is needed on this path; the LP kernel above remains the solver of
 // the relaxation (int_mode relax) and of the relaxation-then-round variant (round_lp).
 // ======================================================================================
-constexpr int NB_CAP = 336;          // DP buckets per chain (config ranges need <= ~327 at any dt)
-constexpr int NBND = 8;              // box-boundary buckets per stage (dp_zspace; 4-5 in practice)
-
-constexpr int NF = NB_CAP;          // exact front DP: labels per stage (dp_front)
-constexpr int NTB = 256;             // key buckets and cost buckets per stage (dp_front)
 
 struct LdsD {
     double *draw, *oat, *ghi, *price;   // [H+1]
@@ -2321,6 +2311,52 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     return 1;
 }
 
+DEV bool round_duties(const Home& h, const Lds& L, int lane, uint16_t* par) {
+    const int H = h.H;
+    // coefficient arrays live in L.yeq / L.zeq / L.yeqp (4H each, free after the ADMM); the
+    // front DP's arrays in the KKT factor blocks Lf / Df (128 H doubles)
+    double* cA = L.yeq;
+    double* cC = L.zeq;
+    double* cq = L.yeqp;
+    double* f = L.Lf;
+    FrontBufs B;
+    B.fa = reinterpret_cast<double2*>(f); f += 2 * NF;
+    B.fb = reinterpret_cast<double2*>(f); f += 2 * NF;
+    B.kb = reinterpret_cast<unsigned long long*>(f); f += NTB;
+    B.cb = reinterpret_cast<unsigned long long*>(f); f += NTB;
+    B.mh = reinterpret_cast<unsigned*>(f); f += NTB / 2;
+    B.kl = reinterpret_cast<unsigned*>(f); f += NTB / 2;
+    B.flo = reinterpret_cast<float*>(f); f += (H + 2) / 2;
+    B.fhi = reinterpret_cast<float*>(f); f += (H + 2) / 2;
+    B.cA = cA; B.cC = cC; B.cq = cq; B.x = L.x; B.par = par;
+    const bool front = h.S == 6 && par != nullptr && (f - L.Lf) <= 128 * H;
+    for (int k = lane; k < H; k += WAVE) {
+        cA[k] = h.aT;
+        cC[k] = L.oat[k + 1] * h.iR * 3600 * h.inv_c;
+        cq[k] = L.q[k * 8 + S_U];
+    }
+    __syncthreads();
+    int r = front ? dp_front<6>(B, H, lane, h.g, h.T0, h.Tmin, h.Tmax, h.Tmin, h.Tmax, S_T, S_U) : -1;
+    if (r < 0) {
+        DpChain cT{H, h.S, S_T, S_U, h.g, cA, cC, h.T0};
+        if (!dp_chain(h, L, cT, lane)) return false;
+    } else if (r == 0) {
+        return false;
+    }
+    for (int k = lane; k < H; k += WAVE) {
+        const double df = L.draw[k + 1] / h.V, rem = 1 - df, d15 = df * TAP;
+        cA[k] = rem + (-rem * h.iRw) * 3600 * h.inv_w;
+        cC[k] = h.e * L.x[k * 8 + S_T] + (d15 + ((-d15) * h.iRw) * 3600 * h.inv_w);
+        cq[k] = L.q[k * 8 + S_W];
+    }
+    __syncthreads();
+    // the tank's stage-0 box is tightened by temp_wh's bounds (build(): lo/hi of slot S_TW)
+    r = front ? dp_front<6>(B, H, lane, h.f, h.Tw0, L.lo[S_TW], L.hi[S_TW], h.Twmin, h.Twmax, S_TW, S_W) : -1;
+    if (r >= 0) return r == 1;
+    DpChain cW{H, h.S, S_TW, S_W, h.f, cA, cC, h.Tw0};
+    return dp_chain(h, L, cW, lane);
+}
+
 // --------------------------------------------------------------------------------------
 // Battery LP (mpc_calc.py:355-373 with its p_grid / cost terms): min sum_k q_k (ch_k + dis_k),
 // E_{k+1} = E_k + a ch_k + b dis_k (a = eta_c/dt, b = 1/(eta_d dt)), 0 <= ch <= r,
@@ -2607,7 +2643,9 @@ __global__ void noise_kernel(int N, int H, uint64_t seed, int off, int stride, i
 bool direct_mode(const dragg_mpc_dims* d) { return d->int_mode == DRAGG_INT_ROUND; }
 
 size_t workspace_bytes(const dragg_mpc_dims* d) {
-    // [N][H][NB_CAP] u16 back-pointers, [N][8H] f64 solutions, [N] i32 DM_BUCKET flags
+    // direct: [N][H][NB_CAP] u16 back-pointers, [N][8H] f64 solutions, [N] i32 DM_BUCKET flags;
+    // round_lp: the back-pointers of its front DP
+    if (d->int_mode == DRAGG_INT_ROUND_LP) return par_region_bytes(d->n_homes, d->horizon);
     return direct_mode(d) ? par_region_bytes(d->n_homes, d->horizon) + (size_t)d->n_homes * 8 * d->horizon * 8 +
                                 (size_t)d->n_homes * sizeof(int)
                           : 0;

@@ -29,13 +29,13 @@ def _exact():
         return json.load(f)
 
 
-def _solve(d):
+def _solve(d, mode="round"):
     import torch
     from dragg_amd import _lib as L
     from dragg_amd.mpc import MPCBatch
     recs = d["records"]
     homes, ex = F.explicit_inputs(d, recs)
-    b = MPCBatch(homes, int_mode="round")
+    b = MPCBatch(homes, int_mode=mode)
     fc, vals = F.prev_hash_arrays(recs, b.H, L.FC_KEYS, L.VAL_KEYS)
     b.fc.copy_(torch.tensor(fc))
     b.vals.copy_(torch.tensor(vals))
@@ -55,13 +55,16 @@ def _thermal_cost(r, fc, i, S):
     return u, wh, w
 
 
+@pytest.mark.parametrize("mode", ["round", "round_lp"])
 @pytest.mark.parametrize("name", F.scenarios())
-def test_integer_dp_is_exact(name, gpu):
+def test_integer_dp_is_exact(name, mode, gpu):
+    """round: the direct path; round_lp: the relaxation first (ADMM + polish), then the same
+    front DP on the integer duties."""
     from dragg_amd import _lib as L
     from oracle import mpc as M
     d = F.load(name)
     ex = _exact()[name]
-    res = _solve(d)
+    res = _solve(d, mode)
     homes = {h["name"]: h for h in d["homes"]}
     n_exact = n_fallback = 0
     gaps = []
@@ -81,7 +84,8 @@ def test_integer_dp_is_exact(name, gpu):
         ref = e["cost_T"] + e["cost_W"]
         gap = (ours - ref) / max(1.0, abs(ref))
         if e["uniform"]:
-            assert res["path"][i] == 0, (name, i, "exact DP fell back", res["path"][i])
+            if mode == "round":
+                assert res["path"][i] == 0, (name, i, "exact DP fell back", res["path"][i])
             assert abs(gap) <= 1e-9, (name, i, r["name"], r["t"], ours, ref)
             n_exact += 1
         else:
@@ -89,9 +93,11 @@ def test_integer_dp_is_exact(name, gpu):
             gaps.append(gap)
             assert gap >= -1e-9, (name, i, ours, ref)      # never below the exact optimum
     gaps = np.array(gaps)
-    msg = f"{name}: {n_exact} records exact (gap <= 1e-9)"
+    msg = f"{name} {mode}: {n_exact} records exact (gap <= 1e-9)"
     if len(gaps):
         msg += f"; {n_fallback} mixed-sign records on the bucketed fallback: gap max {gaps.max():.2e}, " \
                f"{int((gaps > 1e-9).sum())} above 1e-9"
-        assert gaps.max() <= 0.01
+        # the fallbacks are bucketed approximations: the direct path's (dp_zspace) measures at
+        # rounding level on these fixtures, round_lp's older fixed-grid dp_chain up to 1.4 %
+        assert gaps.max() <= (1e-6 if mode == "round" else 0.02)
     print(msg)

@@ -154,8 +154,8 @@ def test_per_home_facade_matches_batch(gpu):
     from dragg_amd.calc import Community, MPCCalc, manage_home
     d = F.load("c1_h24")
     env = d["env"]
-    com = Community(d["homes"], env["oat"], env["ghi"], env["tou_window"], 0, [0.0] * 24, seed=4)
-    calcs = [MPCCalc(h, com) for h in d["homes"]]
+    com = Community(d["homes"], env["oat"], env["ghi"], env["tou_window"], 0, [0.0] * 24, seed=4).make_default()
+    calcs = [MPCCalc(h) for h in d["homes"]]          # the reference's MPCCalc(home) (mpc_calc.py:25)
     ref = DeviceAggregator(d["homes"], env["oat"], env["ghi"], env["tou_window"], 0, 4, reward_price=[0.0] * 24,
                            seed=4)
     for t in range(4):

@@ -169,3 +169,22 @@ def test_size_queries_without_gpu(lib_path):
     d.horizon = 400                                    # LP kernel's LDS is the binding limit
     d.int_mode = L.INT_RELAX
     assert lib.dragg_mpc_lds_bytes(ctypes.byref(d)) == -4
+
+
+def test_solver_name_plug_point():
+    """home['hems']['solver'] (mpc_calc.py:141-145): every MILP backend name -- and an unknown
+    name, which the reference replaces by GLPK_MI -- selects the exact MILP path; the build's
+    own int_mode names select themselves."""
+    from dragg_amd.calc import int_mode_for
+    for name, mode in (("GLPK_MI", "round"), ("GUROBI", "round"), ("ECOS", "round"), ("nonsense", "round"),
+                       ("relax", "relax"), ("round_lp", "round_lp")):
+        assert int_mode_for({"hems": {"solver": name}}) == mode
+    assert int_mode_for({"hems": {}}) == "round"
+
+
+def test_mpccalc_needs_a_community():
+    """MPCCalc(home) without a community attaches to the default one; with none it raises."""
+    from dragg_amd.calc import Community, MPCCalc
+    Community._default = None
+    with pytest.raises(RuntimeError):
+        MPCCalc({"name": "h", "type": "base", "hems": {"solver": "GLPK_MI"}})
