@@ -1263,6 +1263,21 @@ DEV int prologue(const KArgs& a, Home& h, const Lds& L, const Io& io, int lane, 
     return status_pre;
 }
 
+
+// reload the per-home scalars after a DP so that they need not stay live in registers through it
+DEV void reload_home(Home& h, const KArgs& a, int home, const double* sv) {
+    const int N = a.d.n_homes;
+    h.H = a.d.horizon; h.S = a.d.sub_steps; h.dt = a.d.dt; h.gamma = a.d.discount;
+    h.type = a.p.home_type[home];
+    h.pv = (h.type & 1) != 0;
+    h.batt = (h.type & 2) != 0;
+    h.nrows = h.batt ? 3 : 2;
+    load_params(h, a.p.params, N, home);
+    h.t = (int)sv[0]; h.counter = (int)sv[1]; h.winter = sv[2] != 0.0;
+    h.T0 = sv[3]; h.Tw0 = sv[4]; h.E0 = sv[5];
+    derive(h);
+}
+
 DEV void write_missing(const KArgs& a, int home) {
     a.out.status[home] = DRAGG_ST_ERR_MISSING;
     a.out.iters[home] = 0;
@@ -2175,26 +2190,24 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         // key position: (dx x - key_lo) * ksc with key_lo = dx > 0 ? xl : -xh
         const double kmul = dx * ksc, kadd = -(dx > 0.0 ? xl : -xh) * ksc;
         const double cadd = -clo * csc;
-        double base[NU];
-#pragma unroll
-        for (int u = 0; u < NU; ++u) base[u] = fma(g, (double)u, C);
         auto fixp = [](double y) { return (unsigned)fmax(y, 0.0); };   // y < 2^31 + 1
         auto dn = [](unsigned v) { return max(v, 1u) - 1u; };
+        // children are numbered c = NU * parent + duty and spread over the lanes (a stage
+        // with n labels takes ceil(NU n / 64) passes, not NU ceil(n / 64))
+        const int nc = n * NU;
         // 1. per key bucket the cheapest child (largest key among equally cheap ones), per
         //    cost bucket the largest-key child (cheapest among equal keys), both as
         //    understated bounds (cost up, key down), by 64-bit LDS atomics
-        for (int i = lane; i < n; i += WAVE) {
+        for (int c = lane; c < nc; c += WAVE) {
+            const int i = c / NU, u = c - i * NU;
             const double2 Li = fa[i];
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                const double xc = fma(A, Li.x, base[u]);
-                if (xc >= bl && xc <= bh) {
-                    const double c = fma(q, (double)u, Li.y);
-                    const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(c, csc, cadd));
-                    const unsigned cu = vc + 2u, kd = dn(vk);
-                    atomicMin(&B.kb[min(NTB - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
-                    atomicMax(&B.cb[min(NTB - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
-                }
+            const double xc = fma(A, Li.x, fma(g, (double)u, C));
+            if (xc >= bl && xc <= bh) {
+                const double cc = fma(q, (double)u, Li.y);
+                const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
+                const unsigned cu = vc + 2u, kd = dn(vk);
+                atomicMin(&B.kb[min(NTB - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
+                atomicMax(&B.cb[min(NTB - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
             }
         }
         __syncthreads();
@@ -2237,48 +2250,55 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         //    - its cost bucket's largest-key child Y' likewise
         //    (the per-bucket tests need one strict inequality: X may be the reference)
         int nn = 0;
-        double nxmin = INFINITY, nxmax = -INFINITY, ncmin = INFINITY, ncmax = -INFINITY;
-        for (int p = 0; p * WAVE < n; ++p) {
-            const int i = lane + p * WAVE;
-            const bool have = i < n;
-            const double2 Li = have ? fa[i] : make_double2(0.0, 0.0);
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                const double xc = fma(A, Li.x, base[u]);
-                const double c = fma(q, (double)u, Li.y);
-                bool keep = have && xc >= bl && xc <= bh;
-                if (keep) {
-                    const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(c, csc, cadd));
-                    const int kbk = min(NTB - 1, (int)(vk >> 23)), cbk = min(NTB - 1, (int)(vc >> 23));
-                    const unsigned ku = vk + 2u, cd = dn(vc);
-                    const unsigned long long ky = B.kb[kbk], cy = B.cb[cbk];
-                    const unsigned ycu = (unsigned)(ky >> 32), ykd = ~(unsigned)ky;
-                    const unsigned zkd = (unsigned)(cy >> 32), zcu = ~(unsigned)cy;
-                    const bool d1 = cd >= B.mh[kbk];
-                    const bool d2 = ku <= ykd && cd >= ycu && (ku < ykd || cd > ycu);
-                    const bool d3 = ku <= B.kl[cbk];
-                    const bool d4 = ku <= zkd && cd >= zcu && (ku < zkd || cd > zcu);
-                    keep = !(d1 || d2 || d3 || d4);
-                }
-                const unsigned long long bal = __ballot(keep);
-                const int slot = nn + __popcll(bal & below);
-                nn += __popcll(bal);
-                if (keep && slot < NF) {
-                    fb[slot] = make_double2(xc, c);
-                    B.par[k * NB_CAP + slot] = (uint16_t)(i | (u << 12));
-                    nxmin = fmin(nxmin, xc);
-                    nxmax = fmax(nxmax, xc);
-                    ncmin = fmin(ncmin, c);
-                    ncmax = fmax(ncmax, c);
-                }
+        unsigned kmn = ~0u, kmx = 0u, cmn = ~0u, cmx = 0u;  // survivors' fixed-point ranges
+        for (int c0 = 0; c0 < nc; c0 += WAVE) {
+            const int c = c0 + lane;
+            const bool have = c < nc;
+            const int i = have ? c / NU : 0, u = c - i * NU;
+            const double2 Li = fa[i];
+            const double xc = fma(A, Li.x, fma(g, (double)u, C));
+            const double cc = fma(q, (double)u, Li.y);
+            const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
+            bool keep = have && xc >= bl && xc <= bh;
+            if (keep) {
+                const int kbk = min(NTB - 1, (int)(vk >> 23)), cbk = min(NTB - 1, (int)(vc >> 23));
+                const unsigned ku = vk + 2u, cd = dn(vc);
+                const unsigned long long ky = B.kb[kbk], cy = B.cb[cbk];
+                const unsigned ycu = (unsigned)(ky >> 32), ykd = ~(unsigned)ky;
+                const unsigned zkd = (unsigned)(cy >> 32), zcu = ~(unsigned)cy;
+                const bool d1 = cd >= B.mh[kbk];
+                const bool d2 = ku <= ykd && cd >= ycu && (ku < ykd || cd > ycu);
+                const bool d3 = ku <= B.kl[cbk];
+                const bool d4 = ku <= zkd && cd >= zcu && (ku < zkd || cd > zcu);
+                keep = !(d1 || d2 || d3 || d4);
+            }
+            const unsigned long long bal = __ballot(keep);
+            const int slot = nn + __popcll(bal & below);
+            nn += __popcll(bal);
+            if (keep && slot < NF) {
+                fb[slot] = make_double2(xc, cc);
+                B.par[k * NB_CAP + slot] = (uint16_t)(i | (u << 12));
+                kmn = umin(kmn, vk); kmx = umax(kmx, vk);
+                cmn = umin(cmn, vc); cmx = umax(cmx, vc);
             }
         }
         if (nn == 0) return 0;                       // no child left inside the feasible set
         if (nn > NF) return -1;                      // front overflow
-        xmin = dpp_reduce(nxmin, [](double a, double b) { return fmin(a, b); });
-        xmax = dpp_reduce(nxmax, [](double a, double b) { return fmax(a, b); });
-        cmin = dpp_reduce(ncmin, [](double a, double b) { return fmin(a, b); });
-        cmax = dpp_reduce(ncmax, [](double a, double b) { return fmax(a, b); });
+        // the next stage's state and cost ranges from the survivors' positions: the exact
+        // position V of a value lies in [v - 1, v + 2], widened past the back-conversion's
+        // rounding
+        {
+            const unsigned Kmn = dpp_reduce(kmn, umin), Kmx = dpp_reduce(kmx, umax);
+            const unsigned Cmn = dpp_reduce(cmn, umin), Cmx = dpp_reduce(cmx, umax);
+            const double klo = dx > 0.0 ? xl : -xh;
+            const double k1 = klo + ((double)Kmn - 1.0) / ksc, k2 = klo + ((double)Kmx + 2.0) / ksc;
+            const double x1 = dx > 0.0 ? k1 : -k2, x2 = dx > 0.0 ? k2 : -k1;
+            xmin = x1 - tw(x1);
+            xmax = x2 + tw(x2);
+            const double c1 = clo + ((double)Cmn - 1.0) / csc, c2 = clo + ((double)Cmx + 2.0) / csc;
+            cmin = c1 - tw(c1);
+            cmax = c2 + tw(c2);
+        }
         for (int b = lane; b < NTB; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
         __syncthreads();
         double2* tmp = fa; fa = fb; fb = tmp;
@@ -2486,7 +2506,7 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
 enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1 };
 
 template <bool EXPLICIT, int MODE>
-__global__ __launch_bounds__(WAVE, 2) void mpc_direct_kernel(KArgs a) {   // 2 waves/SIMD: 8 homes per CU
+__global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_kernel(KArgs a) {
     constexpr int NT = WAVE;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int home = blockIdx.x;
@@ -2529,6 +2549,12 @@ __global__ __launch_bounds__(WAVE, 2) void mpc_direct_kernel(KArgs a) {   // 2 w
         twhi0 = fmin(h.Twmax, h.Twmax - Kc);
     }
     int status = presolve_direct(h, D, twlo0, twhi0, lane) ? DRAGG_ST_INFEASIBLE : DRAGG_ST_OPTIMAL;
+    double* const saved = D.sc + 20;                    // step inputs, for reload_home
+    if (lane == 0) {
+        saved[0] = h.t; saved[1] = h.counter; saved[2] = h.winter ? 1.0 : 0.0;
+        saved[3] = h.T0; saved[4] = h.Tw0; saved[5] = h.E0; saved[6] = twlo0; saved[7] = twhi0;
+    }
+    __syncthreads();
     pf.mark(DRAGG_PH_SETUP);
     double obj = NAN;
     int int_path = 0;
@@ -2537,6 +2563,8 @@ __global__ __launch_bounds__(WAVE, 2) void mpc_direct_kernel(KArgs a) {   // 2 w
         // chain 1: water heater given T (mpc_calc.py:330-332).  One DP instantiation for both.
         bool ok = true;
         for (int chain = 0; chain < 2 && ok; ++chain) {
+            reload_home(h, a, home, saved);
+            twlo0 = saved[6]; twhi0 = saved[7];
             for (int k = lane; k < H; k += NT) {
                 const double wk = pow(h.gamma, (double)k) * D.price[k];
                 if (chain == 0) {
@@ -2577,6 +2605,7 @@ __global__ __launch_bounds__(WAVE, 2) void mpc_direct_kernel(KArgs a) {   // 2 w
             }
         }
         pf.mark(DRAGG_PH_INTEGER);
+        reload_home(h, a, home, saved);
         if (!ok) status = DRAGG_ST_ROUND_FAIL;
         if (ok && h.batt) {
             for (int k = lane; k < H; k += NT) D.cq[k] = pow(h.gamma, (double)k) * D.price[k] * h.S;

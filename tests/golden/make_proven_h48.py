@@ -101,12 +101,18 @@ def solve_one(args):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     workers = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-    # homes spread over the community (its type blocks: 40 % base, 20 % each other type)
-    idx = [(i * 9973) % N_COMMUNITY for i in range(n)]
+    # homes spread over the community, the same number of each type (the generator lists them in
+    # blocks: pv_battery, pv_only, battery_only 20 % each, then base 40 %)
+    homes = community()[0]
+    blocks = {}
+    for i, h in enumerate(homes):
+        blocks.setdefault(h["type"], []).append(i)
+    per = n // len(blocks)
+    idx = [b[(j * 397) % len(b)] for b in blocks.values() for j in range(per)]
     jobs = [(h, i % 2, 3600.0) for i, h in enumerate(idx)]
+    jobs.sort(key=lambda j: -j[1])                 # the t = 1 jobs (two solves) first
     with mp.get_context("fork").Pool(workers) as pool:
         recs = pool.map(solve_one, jobs, chunksize=1)
-    homes = community()[0]
     used = sorted({r["home"] for r in recs})
     out = dict(scenario="proven_h48_july", params=dict(community=N_COMMUNITY, seed_homes=SEED_HOMES,
                seed_weather=SEED_WEATHER, month=MONTH, dt=DT, horizon_hours=HH),
