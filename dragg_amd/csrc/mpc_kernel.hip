@@ -2090,6 +2090,11 @@ struct FrontBufs {
     uint16_t* par;                       // [H][NB_CAP] global
 };
 
+// 1 / w to about 1 ulp: v_rcp_f64 and one Newton step (no IEEE division sequence)
+DEV double rcp_nr(double w) {
+    double r = __builtin_amdgcn_rcp(w);
+    return fma(fma(-w, r, 1.0), r, r);
+}
 DEV float f32_down(double v) { float f = (float)v; return (double)f > v ? nextafterf(f, -INFINITY) : f; }
 DEV float f32_up(double v) { float f = (float)v; return (double)f < v ? nextafterf(f, INFINITY) : f; }
 // floats -> u32 with the same order
@@ -2146,7 +2151,8 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         for (int k = H - 1; k >= 1 && !empty; --k) {
             narrow = narrow || (u - l < fabs(g));
             const double A = B.cA[k], C = B.cC[k];
-            const double pl = (l - C - gmax) / A, ph = (u - C - gmin) / A;
+            const double iA = rcp_nr(A);                 // ~1 ulp; tw() below widens past it
+            const double pl = (l - C - gmax) * iA, ph = (u - C - gmin) * iA;
             const double bl = k == 1 ? lo0 : lo, bh = k == 1 ? hi0 : hi;
             l = fmax(pl, bl - tw(bl));
             u = fmin(ph, bh + tw(bh));
@@ -2185,8 +2191,10 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         xl -= tw(xl); xh += tw(xh);
         double clo = cmin + fmin(0.0, q * SS), chi = cmax + fmax(0.0, q * SS);
         clo -= tw(clo); chi += tw(chi);
+        // scales ~ NTB 2^23 / width by a refined reciprocal (any scale near it will do: the
+        // positions are monotone and their bounds hold for the scale actually used)
         const double FX = (double)NTB * 8388608.0;        // NTB * 2^23 <= 2^31
-        const double ksc = FX / (xh - xl), csc = FX / (chi - clo);
+        const double ksc = FX * rcp_nr(xh - xl), csc = FX * rcp_nr(chi - clo);
         // key position: (dx x - key_lo) * ksc with key_lo = dx > 0 ? xl : -xh
         const double kmul = dx * ksc, kadd = -(dx > 0.0 ? xl : -xh) * ksc;
         const double cadd = -clo * csc;
@@ -2291,11 +2299,13 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             const unsigned Kmn = dpp_reduce(kmn, umin), Kmx = dpp_reduce(kmx, umax);
             const unsigned Cmn = dpp_reduce(cmn, umin), Cmx = dpp_reduce(cmx, umax);
             const double klo = dx > 0.0 ? xl : -xh;
-            const double k1 = klo + ((double)Kmn - 1.0) / ksc, k2 = klo + ((double)Kmx + 2.0) / ksc;
+            const double ik = (xh - xl) * (1.0 / FX);     // ~1 / ksc; tw() covers the difference
+            const double k1 = fma((double)Kmn - 1.0, ik, klo), k2 = fma((double)Kmx + 2.0, ik, klo);
             const double x1 = dx > 0.0 ? k1 : -k2, x2 = dx > 0.0 ? k2 : -k1;
             xmin = x1 - tw(x1);
             xmax = x2 + tw(x2);
-            const double c1 = clo + ((double)Cmn - 1.0) / csc, c2 = clo + ((double)Cmx + 2.0) / csc;
+            const double ic = (chi - clo) * (1.0 / FX);
+            const double c1 = fma((double)Cmn - 1.0, ic, clo), c2 = fma((double)Cmx + 2.0, ic, clo);
             cmin = c1 - tw(c1);
             cmax = c2 + tw(c2);
         }
