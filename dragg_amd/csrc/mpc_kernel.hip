@@ -1381,7 +1381,7 @@ struct LdsD {
     // --- tail, a union: dp_front's arrays or dp_zspace's (never live together)
     unsigned long long *kb, *cb;        // [NTB]  dp_front: per key / cost bucket packed extremes
     unsigned *mh, *kl;                  // [NTB]  dp_front: scans of kb / cb
-    float *flo, *fhi;                   // [H+1]  dp_front: feasible-set hull of x_k
+    unsigned *flo, *fhi;                // [H+1]  dp_front: feasible-set hull of x_k (fixed point)
     double2 *cand;                      // [NBND][S+1] boundary-bucket candidates per duty
     double *rt;                         // [H+2] zero-duty reference trajectory of the chain
     int *candp;                         // [NBND][S+1] candidate records
@@ -1473,8 +1473,8 @@ DEV LdsD carve_direct(double* smem, int H, int S) {
     L.cb = reinterpret_cast<unsigned long long*>(b + o.cb);
     L.mh = reinterpret_cast<unsigned*>(b + o.mh);
     L.kl = reinterpret_cast<unsigned*>(b + o.kl);
-    L.flo = reinterpret_cast<float*>(b + o.flo);
-    L.fhi = reinterpret_cast<float*>(b + o.fhi);
+    L.flo = reinterpret_cast<unsigned*>(b + o.flo);
+    L.fhi = reinterpret_cast<unsigned*>(b + o.fhi);
     L.cand = reinterpret_cast<double2*>(b + o.cand);
     L.rt = D(o.rt);
     L.candp = reinterpret_cast<int*>(b + o.candp);
@@ -2084,7 +2084,8 @@ struct FrontBufs {
     unsigned long long* cb;              // [NTB] cost buckets: packed (key down | ~cost up) maxima
     unsigned* mh;                        // [NTB] ordered min cost over the key buckets above
     unsigned* kl;                        // [NTB] ordered max key over the cost buckets below
-    float *flo, *fhi;                    // [H + 1] feasible-set hull of x_k
+    unsigned *flo, *fhi;                 // [H + 1] feasible-set hull of x_k: 32-bit fixed point
+                                         //   over the chain's widened box, rounded outward
     const double *cA, *cC, *cq;          // [H] chain coefficients and duty costs
     double* x;                           // [8H] stage-slot solution (writes slots sx, sv)
     uint16_t* par;                       // [H][NB_CAP] global
@@ -2094,13 +2095,6 @@ struct FrontBufs {
 DEV double rcp_nr(double w) {
     double r = __builtin_amdgcn_rcp(w);
     return fma(fma(-w, r, 1.0), r, r);
-}
-DEV float f32_down(double v) { float f = (float)v; return (double)f > v ? nextafterf(f, -INFINITY) : f; }
-DEV float f32_up(double v) { float f = (float)v; return (double)f < v ? nextafterf(f, INFINITY) : f; }
-// floats -> u32 with the same order
-DEV unsigned ord32(float v) {
-    const unsigned b = __float_as_uint(v);
-    return (b >> 31) ? ~b : (b | 0x80000000u);
 }
 // inclusive scan over the 64 lanes with identity id (lanes shifted in from outside a row
 // keep id: bound_ctrl off), rows combined through v_readlane
@@ -2140,13 +2134,21 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     neg = __any(neg);
     if (pos && neg) return -1;
     const double dx = ((g > 0.0) != neg) ? 1.0 : -1.0;
-    // (b) feasible-set hulls F_H .. F_1 (every lane computes, lane 0 stores)
+    // (b) feasible-set hulls F_H .. F_1 (every lane computes, lane 0 stores).  Stored as 32-bit
+    //     fixed point over [hb, hb + 2^32 hs], a range past every stage box and its tolerance
+    //     (values outside it would be cut by the stage box anyway): lower ends rounded down,
+    //     upper ends up, so the stored hull contains the computed one (one unit ~ box / 2^32)
+    const double hb0 = fmin(lo0, lo), he0 = fmax(hi0, hi);
+    const double hb = hb0 - 4.0 * tw(hb0), hw = (he0 + 4.0 * tw(he0)) - hb;
+    const double hs = hw * 0x1p-32, his = 0x1p32 * rcp_nr(hw);
+    auto enc_lo = [&](double v) { return (unsigned)fmin(fmax((v - hb) * his, 0.0), 4294967295.0); };
+    auto enc_hi = [&](double v) { return (unsigned)fmin(fmax((v - hb) * his + 1.0, 0.0), 4294967295.0); };
     {
         bool empty = false, narrow = false;
         double l = H == 1 ? lo0 : lo, u = H == 1 ? hi0 : hi;
         l -= tw(l);
         u += tw(u);
-        if (lane == 0) { B.flo[H] = f32_down(l); B.fhi[H] = f32_up(u); }
+        if (lane == 0) { B.flo[H] = enc_lo(l); B.fhi[H] = enc_hi(u); }
         const double gmin = fmin(0.0, g * SS), gmax = fmax(0.0, g * SS);
         for (int k = H - 1; k >= 1 && !empty; --k) {
             narrow = narrow || (u - l < fabs(g));
@@ -2159,7 +2161,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             l -= tw(l);
             u += tw(u);
             empty = l > u;
-            if (lane == 0) { B.flo[k] = f32_down(l); B.fhi[k] = f32_up(u); }
+            if (lane == 0) { B.flo[k] = enc_lo(l); B.fhi[k] = enc_hi(u); }
         }
         if (empty) return 0;
         if (narrow) return -1;
@@ -2178,7 +2180,10 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         double bl = k == 0 ? lo0 : lo, bh = k == 0 ? hi0 : hi;
         bl -= tw(bl);
         bh += tw(bh);
-        if (k + 1 < H) { bl = fmax(bl, (double)B.flo[k + 1]); bh = fmin(bh, (double)B.fhi[k + 1]); }
+        if (k + 1 < H) {
+            bl = fmax(bl, fma((double)B.flo[k + 1], hs, hb));
+            bh = fmin(bh, fma((double)B.fhi[k + 1], hs, hb));
+        }
         // the children's state and cost ranges (widened past rounding) define the two bucket
         // grids of this stage.  A child's position in a range as a 32-bit fixed-point number
         // v = (key - lo) * NTB * 2^23 / (hi - lo) (one fma from the state) gives its bucket
@@ -2356,8 +2361,8 @@ DEV bool round_duties(const Home& h, const Lds& L, int lane, uint16_t* par) {
     B.cb = reinterpret_cast<unsigned long long*>(f); f += NTB;
     B.mh = reinterpret_cast<unsigned*>(f); f += NTB / 2;
     B.kl = reinterpret_cast<unsigned*>(f); f += NTB / 2;
-    B.flo = reinterpret_cast<float*>(f); f += (H + 2) / 2;
-    B.fhi = reinterpret_cast<float*>(f); f += (H + 2) / 2;
+    B.flo = reinterpret_cast<unsigned*>(f); f += (H + 2) / 2;
+    B.fhi = reinterpret_cast<unsigned*>(f); f += (H + 2) / 2;
     B.cA = cA; B.cC = cC; B.cq = cq; B.x = L.x; B.par = par;
     const bool front = h.S == 6 && par != nullptr && (f - L.Lf) <= 128 * H;
     for (int k = lane; k < H; k += WAVE) {

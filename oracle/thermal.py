@@ -176,3 +176,30 @@ def brute_force(ch):
             if best is None or c < best:
                 best = c
     return best
+
+
+def exact_milp(hc, si, th="solve"):
+    """The optimum of the reference's whole MILP (`mpc_calc.py:291-451`) for one solve, or None
+    if it is infeasible: the integer columns fixed to the exact thermal schedule `th`
+    (`thermal_optimum`, computed here unless given), the remaining columns (battery, PV, grid,
+    cost) solved as an LP by HiGHS.  The model is separable (no row
+    couples the duty columns with the battery / PV columns, only the linear objective), so the
+    LP optimum is the MILP optimum; tests/test_oracle_thermal.py pins this against every
+    fixture record HiGHS proved optimal or infeasible."""
+    from scipy.optimize import linprog
+    from oracle import mpc as M
+    if isinstance(th, str):
+        th = thermal_optimum(hc, si)
+    if th is None:
+        return None
+    P = M.build_problem(hc, si)
+    Lay = P["layout"]
+    n = P["c"].shape[0]
+    lb, ub = np.full(n, -np.inf), np.full(n, np.inf)
+    on, off = ("hvac_heat_on", "hvac_cool_on") if si.winter else ("hvac_cool_on", "hvac_heat_on")
+    for key, vals in ((on, th["u_T"]), (off, np.zeros(hc.H)), ("wh_heat_on", th["u_W"])):
+        o = Lay.off[key]
+        lb[o:o + hc.H] = ub[o:o + hc.H] = np.asarray(vals, float)
+    res = linprog(P["c"], A_ub=P["A_ub"], b_ub=P["b_ub"], A_eq=P["A_eq"], b_eq=P["b_eq"],
+                  bounds=list(zip(lb, ub)), method="highs")
+    return float(res.fun) if res.status == 0 else None

@@ -5,8 +5,13 @@ For every record of tests/golden/*.json.gz and tests/golden/proven/*.json.gz, so
 reference's thermal integer programme with oracle/thermal.py (assumption-free backward
 step-function DP, itself pinned by tests/test_oracle_thermal.py against enumeration and HiGHS)
 and writes tests/golden/proven/thermal_exact.json.gz: per scenario and record the exact
-indoor-air and tank chain costs (None where a chain has no integer schedule), plus whether the
-record's duty prices have one sign (where the GPU's Pareto-front DP applies).  The GPU test
+indoor-air and tank chain costs (None where a chain has no integer schedule), whether the
+record's duty prices have one sign (where the GPU's Pareto-front DP applies), and the EXACT
+optimum of the whole MILP ("opt_obj"): the reference model (oracle/mpc.py build_problem) with its
+integer columns fixed to the exact thermal schedule, the rest (battery, PV, grid, cost) solved as
+an LP by HiGHS (oracle/thermal.py exact_milp).  The MILP is separable (the battery and PV columns share
+no row with the duty columns, only the linear objective), so this LP optimum is the MILP optimum;
+tests/test_oracle_thermal.py checks that claim against every record HiGHS proved optimal.  The GPU test
 tests/test_gpu_exact.py compares the kernel's integer solutions with these numbers, so the GPU
 box needs neither the oracle run nor scipy.
 
@@ -51,7 +56,9 @@ def main():
             uniform = bool(np.all(chT["q"] >= 0) or np.all(chT["q"] <= 0))
             T = TH.solve_chain(chT)
             W = TH.solve_chain(TH.chain_W(hc, si, T[2])) if T is not None else None
-            rows.append(dict(uniform=uniform, cost_T=None if T is None else T[0], cost_W=None if W is None else W[0]))
+            th = None if W is None else dict(u_T=T[1], u_W=W[1])
+            rows.append(dict(uniform=uniform, cost_T=None if T is None else T[0], cost_W=None if W is None else W[0],
+                             opt_obj=TH.exact_milp(hc, si, th)))
         out[name] = rows
         n_ok = sum(1 for x in rows if x["cost_W"] is not None)
         print(f"{name}: {len(rows)} records, {n_ok} with an integer schedule", flush=True)

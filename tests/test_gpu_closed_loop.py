@@ -6,8 +6,12 @@ noise the reference drew at every (home, step), all `num_timesteps` steps chaine
 the device-resident hash.  The collected series must match the reference's results.json.
 
 Where the reference's solver returned a HiGHS incumbent (c1_h24: 5 s MILP limit, §2 of
-DESIGN.md) our exact optimum can differ and the closed loop then departs from the
-reference's path for that home; those homes are counted and bounded, the rest must match."""
+DESIGN.md) our exact optimum can differ, and where the MILP has several optimal schedules ours
+may be another one; the closed loop then departs from the reference's path for that home.  Every
+departure must be explained by the solve where it starts (the first step whose series differ,
+whose inputs are still the reference's): the exact MILP optimum there
+(tests/golden/proven/thermal_exact.json.gz, which the kernel reaches -- test_gpu_parity.py) is
+below the reference's incumbent, or ties with the reference's objective."""
 import numpy as np
 import pytest
 
@@ -15,8 +19,17 @@ from tests import fixtures as F
 
 pytestmark = pytest.mark.gpu
 
-# scenario -> homes whose closed loop may depart from the reference (HiGHS incumbents)
-ALLOWED_DEPARTURES = {"c1_h24": 20}
+
+
+def _first_departure(a, b):
+    """First step at which any series of a home differs (None: the home follows)."""
+    first = None
+    for k in b:
+        if isinstance(b[k], list):
+            bad = np.flatnonzero(~np.isclose(a[k], b[k], rtol=1e-6, atol=1e-6))
+            if len(bad):
+                first = int(bad[0]) if first is None else min(first, int(bad[0]))
+    return first
 
 
 def _windows(d):
@@ -53,20 +66,33 @@ def test_closed_loop_matches_reference_results(gpu, name):
     torch.cuda.synchronize()
     got = dev.collected_data()
     ref = d["results"]
-    departed = []
+    from tests.test_gpu_parity import _exact
+    ex = _exact(name)
+    rec = {(r["t"], r["name"]): (i, r) for i, r in enumerate(d["records"])}
+    departed, incumbent, tie = [], 0, 0
     for h in homes:
         a, b = got[h["name"]], ref[h["name"]]
         assert list(a) == list(b)
-        ok = True
         for k in b:
             if isinstance(b[k], list):
                 assert len(a[k]) == len(b[k]), (h["name"], k)
-                if not np.allclose(a[k], b[k], rtol=1e-6, atol=1e-6):
-                    ok = False
-        if not ok:
-            departed.append(h["name"])
+        t0 = _first_departure(a, b)
+        if t0 is None:
+            continue
+        departed.append((h["name"], t0))
+        i, r = rec[(t0, h["name"])]
+        opt, ro = ex[i]["opt_obj"], r["milp_obj"]
+        assert opt is not None and ro is not None, (name, h["name"], t0, r["status"])
+        rel = (opt - ro) / max(1.0, abs(ro))
+        assert rel <= 2e-6, (name, h["name"], t0, opt, ro)      # never above the reference's solve
+        if rel < -2e-6:
+            assert r["milp_status"] != 0, (name, h["name"], t0)  # a proven optimum cannot be beaten
+            incumbent += 1
+        else:
+            tie += 1
     loads = R.aggregate_loads(dev.hist[:T].cpu().numpy())
     close = np.isclose(loads, ref["Summary"]["p_grid_aggregate"], rtol=1e-6, atol=1e-6)
     print(f"{name}: {len(homes) - len(departed)}/{len(homes)} homes follow the reference's closed loop "
-          f"over {T} steps; community load equal (1e-6) at {int(close.sum())}/{T} steps")
-    assert len(departed) <= ALLOWED_DEPARTURES.get(name, 0), departed
+          f"over {T} steps; community load equal (1e-6) at {int(close.sum())}/{T} steps; departures "
+          f"{departed}: {incumbent} start where the reference kept a suboptimal incumbent, {tie} at an "
+          f"alternative optimum")

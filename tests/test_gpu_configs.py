@@ -1,0 +1,205 @@
+"""BASELINE configs[1], [3] and [4] at their own sizes on one GPU (configs[2] is
+tests/test_gpu_fullsize.py and the bench).
+
+The CPU oracle cannot solve these runs, but it can check any answer the HIP path gives, so each
+test runs the whole workload on the device and then checks a sample of its solves on the host:
+
+* the state a sampled solve started from is restated by the oracle from the previous step's
+  hash (water draws, initial conditions, environment slices, the device's season draw);
+* the exact MILP optimum of that state (oracle/thermal.py exact_milp: the thermal DP + the LP of the
+  rest with the duties fixed; pinned on every HiGHS-proven fixture record by
+  tests/test_oracle_thermal.py) decides the status -- ours optimal iff it exists -- and the
+  objective must equal it (1e-6 relative);
+* the written answer satisfies the reference model (violation <= 1e-5, duties integral,
+  c.x = objective).
+
+Synthetic communities can contain battery homes whose t = 0 solve fails; the reference then
+raises KeyError('e_batt_opt') at t = 1 (mpc_calc.py:280-289).  Such a run is not one the
+reference completes: the tests assert that check_errors() raises exactly that, and that every
+such home is a battery home whose t = 0 solve failed.
+"""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _community(n, hours, dt, steps, month, seed):
+    from dragg_amd.community import synthetic_homes, synthetic_weather
+    sim_hours = math.ceil(steps / dt)
+    days = math.ceil((sim_hours + hours + 2) / 24) + 1
+    homes = synthetic_homes(n, seed=seed, days=days, dt=dt, horizon_hours=hours)
+    oat, ghi, tou = synthetic_weather(days, dt, sim_hours, seed=seed + 1, month=month)
+    return homes, oat, ghi, tou
+
+
+def _check_sample(homes, oat, ghi, tou, rp, t, prev_vals, prev_fc, noise, status, obj, vals, fc, pick):
+    """Exact optimum + reference-model check of the solves `pick` of step t."""
+    from oracle import mpc as M
+    from oracle import thermal as TH
+    from dragg_amd import _lib as L
+    from tests.test_gpu_fullsize import _hash_dict
+    from tests.test_gpu_parity import _expand
+    worst_gap = worst_v = 0.0
+    n_opt = n_none = 0
+    for i in pick:
+        hc = M.home_const(homes[i])
+        draw, _, _ = M.water_draws(hc, t)
+        T0, Tw0, E0, _ = M.initial_conditions(hc, t, _hash_dict(prev_vals, prev_fc, i) if t else {}, draw)
+        o, g, tt = M.env_slice(oat, ghi, tou, 0, t, hc.H)
+        si = M.StepInput(t=t, T0=T0, Tw0=Tw0, E0=E0, oat=o, ghi=g, price=M.total_price(tt, rp, hc.H), draw=draw,
+                         winter=M.season_is_winter(o, noise[:, i]))
+        opt = TH.exact_milp(hc, si)
+        ours = status[i] == L.ST_OPTIMAL
+        assert ours == (opt is not None), (t, i, homes[i]["type"], L.STATUS_NAMES[status[i]], opt)
+        if not ours:
+            n_none += 1
+            continue
+        n_opt += 1
+        gap = abs(obj[i] - opt) / max(1.0, abs(opt))
+        worst_gap = max(worst_gap, gap)
+        assert gap <= 1e-6, (t, i, homes[i]["type"], obj[i], opt)
+        P, x = _expand(hc, si, vals[:, i], fc[:, :, i], hc.S)
+        ve = np.abs(P["A_eq"] @ x - P["b_eq"]).max()
+        vu = (P["A_ub"] @ x - P["b_ub"]).max()
+        worst_v = max(worst_v, ve, vu)
+        assert ve <= 1e-5 and vu <= 1e-5, (t, i, ve, vu)
+        duties = x[P["integrality"] == 1]
+        assert np.array_equal(duties, np.round(duties)), (t, i)
+        assert abs(P["c"] @ x - obj[i]) <= 1e-8 * max(1, abs(obj[i])), (t, i)
+    return n_opt, n_none, worst_gap, worst_v
+
+
+def _errors_are_the_references(agg, homes):
+    """check_errors() raises iff a home hit a crashing path, and each such home is a battery home
+    whose t = 0 solve failed (the reference's KeyError('e_batt_opt') at t = 1)."""
+    from dragg_amd import _lib as L
+    st = agg.status_hist[:agg.timestep].cpu().numpy()
+    miss = np.argwhere(st == L.ST_ERR_MISSING)
+    assert not (st == L.ST_ERR_PARSE).any()
+    if len(miss) == 0:
+        agg.check_errors()
+        return 0
+    with pytest.raises(KeyError):
+        agg.check_errors()
+    for _, i in miss:
+        assert "battery" in homes[agg.index[i]]["type"]
+        assert st[0, i] != L.ST_OPTIMAL
+    return len(np.unique(miss[:, 1]))
+
+
+def _sample(rng, status, homes, per_type):
+    """per_type solves of each home type, drawn from the optimal ones and the others alike."""
+    types = np.array([h["type"] for h in homes])
+    out = []
+    for ty in ("base", "pv_only", "battery_only", "pv_battery"):
+        idx = np.flatnonzero(types == ty)
+        out.extend(rng.choice(idx, min(per_type, len(idx)), replace=False))
+    return np.array(out)
+
+
+def _run(n, hours, dt, steps, month, seed, sample_steps, per_type, rp=(0.0,), keep_history=True):
+    import torch
+    from dragg_amd.aggregator import DeviceAggregator
+    homes, oat, ghi, tou = _community(n, hours, dt, steps, month, seed)
+    agg = DeviceAggregator(homes, oat, ghi, tou, 0, steps, reward_price=list(rp), seed=seed,
+                           keep_history=keep_history)
+    rng = np.random.default_rng(seed)
+    checked = []
+    for t in range(steps):
+        b = agg.batch
+        snap = (t in sample_steps) and (b.vals.clone(), b.fc.clone(), b.season_noise(t).cpu().numpy())
+        agg.run_iteration()
+        agg.collect_data(defer=True)
+        if snap:
+            torch.cuda.synchronize()
+            st, ob = b.status.cpu().numpy(), b.obj.cpu().numpy()
+            pick = _sample(rng, st, homes, per_type)
+            res = _check_sample(homes, oat, ghi, tou, list(rp), t, snap[0].cpu().numpy(), snap[1].cpu().numpy(),
+                                snap[2], st, ob, b.vals.cpu().numpy(), b.fc.cpu().numpy(), pick)
+            checked.append((t,) + res)
+    agg.reduce_history()
+    torch.cuda.synchronize()
+    return homes, agg, checked
+
+
+def _report(tag, agg, homes, checked):
+    from dragg_amd import _lib as L
+    st = agg.status_hist[:agg.timestep].cpu().numpy()
+    counts = {L.STATUS_NAMES[c]: int((st == c).sum()) for c in np.unique(st)}
+    n_err = _errors_are_the_references(agg, homes)
+    n_opt = sum(c[1] for c in checked)
+    n_none = sum(c[2] for c in checked)
+    print(f"{tag}: {st.size} solves {counts}; homes on the reference's KeyError path: {n_err}; "
+          f"checked {n_opt} optimal solves (|gap| to the exact MILP optimum max "
+          f"{max(c[3] for c in checked):.1e}, violation max {max(c[4] for c in checked):.1e}) and "
+          f"{n_none} without an integer schedule")
+    assert n_opt >= 50
+    return st
+
+
+def test_config1_1k_homes_h24_96_steps(gpu):
+    """configs[1]: 1,000 homes, run_rbo_mpc, 24 h at 15-min steps, 6 h horizon."""
+    homes, agg, checked = _run(1000, 6, 4, 96, 1, 31, sample_steps={0, 1, 23, 47, 95}, per_type=25)
+    st = _report("configs[1] 1k homes x 96 steps, H = 24, January", agg, homes, checked)
+    assert st.shape == (96, 1000)
+    # the collected sums are the homes' fields summed (aggregator.py:728-755)
+    from dragg_amd import _lib as L
+    hist = agg.hist[:96].cpu().numpy()
+    want = np.stack([hist[:, L.K[k], :].sum(axis=1) for k in ("p_grid_opt", "forecast_p_grid_opt", "cost_opt")], 1)
+    got = agg.agg_hist[:96].cpu().numpy()
+    ok = ~np.isnan(want)
+    assert np.allclose(got[ok], want[ok], rtol=1e-12, atol=1e-9)
+
+
+def test_config3_100k_homes_7_days(gpu):
+    """configs[3]: 100,000 homes, 7 days at 15-min steps (672 steps), device-resident state,
+    no per-step history (keep_history=False)."""
+    homes, agg, checked = _run(100000, 6, 4, 672, 7, 41, sample_steps={0, 335, 671}, per_type=20,
+                               keep_history=False)
+    assert agg.hist is None
+    st = _report("configs[3] 100k homes x 672 steps, H = 24, July", agg, homes, checked)
+    assert st.shape == (672, 100000)
+    assert np.isfinite(agg.agg_hist[:672].cpu().numpy()[:, 0]).all()
+
+
+def test_config4_rl_10k_homes_price_broadcast_and_rollouts(gpu):
+    """configs[4]: run_rl_agg at 10,000 homes (H = 48): per action the reward price is set,
+    forecast_horizon rollout steps are solved and the state restored, then the committed steps
+    must equal the rollout bit for bit; a sample of the committed RL-price solves is checked
+    against the exact optimum (prices of either sign: the kernel's mixed-sign path included)."""
+    import torch
+    from dragg_amd.aggregator import DeviceAggregator
+    homes, oat, ghi, tou = _community(10000, 12, 4, 8, 7, 51)
+    agg = DeviceAggregator(homes, oat, ghi, tou, 0, 8, reward_price=[0.0] * 48, seed=51)
+    for _ in range(2):
+        agg.run_iteration()
+        agg.collect_data()
+    rp = list(-0.03 * np.cos(np.arange(48) / 3.0))
+    agg.set_reward_price(rp)
+    snap = agg.snapshot()
+    fc = agg.forecast(2)
+    after = agg.snapshot()
+    assert after[0] == snap[0]
+    assert torch.equal(after[1].nan_to_num(7.7), snap[1].nan_to_num(7.7))
+    assert torch.equal(after[2].nan_to_num(7.7), snap[2].nan_to_num(7.7))
+    b = agg.batch
+    t = agg.timestep
+    prev_vals, prev_fc, noise = b.vals.cpu().numpy(), b.fc.cpu().numpy(), b.season_noise(t).cpu().numpy()
+    committed = []
+    for s in range(2):
+        agg.run_iteration()
+        committed.append(agg.collect_data().clone())
+        if s == 0:
+            torch.cuda.synchronize()
+            st, ob = b.status.cpu().numpy(), b.obj.cpu().numpy()
+            pick = _sample(np.random.default_rng(51), st, homes, 25)
+            res = _check_sample(homes, oat, ghi, tou, rp, t, prev_vals, prev_fc, noise, st, ob,
+                                b.vals.cpu().numpy(), b.fc.cpu().numpy(), pick)
+    assert torch.equal(fc, torch.stack(committed))
+    agg.restore(snap)
+    agg.set_reward_price([x + 0.2 for x in rp])
+    assert not torch.equal(agg.forecast(1), fc[:1])
+    _report("configs[4] RL 10k homes, H = 48, July, rollout = commit", agg, homes, [(t,) + res])

@@ -69,3 +69,69 @@ def test_exact_thermal_matches_reference_milp_on_base_homes(name):
             assert th["cost"] <= ref + 2e-6 * max(1.0, abs(ref)), (name, r["name"], r["t"], th["cost"], ref)
     assert n_proven >= 5
     print(f"{name}: {n_proven} proven base-home optima reproduced, {n_incumbent} incumbents not beaten")
+
+
+def _exact_fixture():
+    import gzip
+    import json
+    import os
+    with gzip.open(os.path.join(F.GOLDEN, "proven", "thermal_exact.json.gz"), "rt") as f:
+        return json.load(f)
+
+
+def _records(name):
+    import gzip
+    import json
+    import os
+    if name.startswith("proven/"):
+        with gzip.open(os.path.join(F.GOLDEN, name + ".json.gz"), "rt") as f:
+            return json.load(f)
+    return F.load(name)
+
+
+def test_exact_milp_optimum_pinned_by_highs():
+    """The exact MILP optimum of every fixture solve (thermal DP + the LP of the rest with the
+    duties fixed, make_thermal_exact.py) against the reference's HiGHS solves, all home types:
+    equal to every PROVEN optimum (2e-6), None on every proven-infeasible record, and never
+    above a time-limited incumbent.  This pins the separability argument (DESIGN.md section
+    3.1) and the sequential tank-after-air solve on the full reference model."""
+    ex = _exact_fixture()
+    n = dict(proven=0, infeasible=0, incumbent=0, better=0)
+    for name, rows in ex.items():
+        d = _records(name)
+        assert len(rows) == len(d["records"])
+        for r, e in zip(d["records"], rows):
+            ms, mo = r["milp_status"], r["milp_obj"]
+            if ms == 2:
+                n["infeasible"] += 1
+                assert e["opt_obj"] is None, (name, r["name"], r["t"])
+            elif mo is not None:
+                assert e["opt_obj"] is not None, (name, r["name"], r["t"])
+                rel = (e["opt_obj"] - mo) / max(1.0, abs(mo))
+                if ms == 0:
+                    n["proven"] += 1
+                    assert abs(rel) <= 2e-6, (name, r["name"], r["t"], e["opt_obj"], mo)
+                else:
+                    n["incumbent"] += 1
+                    n["better"] += rel < -2e-6
+                    assert rel <= 2e-6, (name, r["name"], r["t"], e["opt_obj"], mo)
+    assert n["proven"] >= 900 and n["infeasible"] >= 400
+    print(f"exact MILP optimum: {n['proven']} proven optima reproduced, {n['infeasible']} proven-infeasible "
+          f"agreed, {n['incumbent']} incumbents never beaten by them ({n['better']} improved on)")
+
+
+def test_exact_fixture_recomputes():
+    """A sample of thermal_exact.json.gz recomputed from the oracle (the file is what it says)."""
+    ex = _exact_fixture()
+    rng = np.random.default_rng(5)
+    for name, rows in ex.items():
+        d = _records(name)
+        homes = {h["name"]: h for h in d["homes"]}
+        for i in rng.choice(len(rows), size=min(6, len(rows)), replace=False):
+            r, e = d["records"][i], rows[i]
+            hc = M.home_const(homes[r["name"]])
+            th = TH.thermal_optimum(hc, _si(r))
+            opt = TH.exact_milp(hc, _si(r), th)
+            assert (opt is None) == (e["opt_obj"] is None), (name, i)
+            if opt is not None:
+                assert opt == pytest.approx(e["opt_obj"], rel=1e-12, abs=1e-12), (name, i)
