@@ -27,7 +27,9 @@ constexpr int RS = 4;        // row stride per stage in LDS
 constexpr int WAVE = 64;
 constexpr int NB_CAP = 336;          // DP buckets per chain (config ranges need <= ~327 at any dt)
 constexpr int NBND = 8;              // box-boundary buckets per stage (dp_zspace; 4-5 in practice)
-constexpr int NF = NB_CAP;          // exact front DP: labels per stage (dp_front)
+constexpr int NF = NB_CAP;              // front capacity (labels) of dp_front
+constexpr int NF_BOUND = 240;           // ... when the LP bound is on: its W table follows the front
+static_assert((NB_CAP + 8 - NF_BOUND) * 16 >= 3 * 64 * 8, "the W table lives in rmin past the front");
 constexpr int NTB = 256;             // key buckets and cost buckets per stage (dp_front)
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
 
@@ -1012,7 +1014,7 @@ DEV bool dp_chain(const Home& h, const Lds& L, const DpChain& c, int lane) {
 
 template <int SS>
 DEV int dp_front(const struct FrontBufs& B, int H, int lane, double g, double x0, double lo0, double hi0, double lo,
-                 double hi, int sx, int sv);
+                 double hi, int sx, int sv, bool use_bound = false);
 
 // int_mode round_lp: the integer duties after the relaxation, by the exact front DP (the
 // default path's, dp_front) with its buffers in the KKT-factor LDS the ADMM no longer needs
@@ -1407,6 +1409,12 @@ __host__ __device__ inline bool direct_fits(int H) { return seg_cap(H) <= NB_CAP
 __host__ __device__ inline size_t par_region_bytes(int N, int H) {
     return ((size_t)N * H * NB_CAP * sizeof(uint16_t) + 255) / 256 * 256;
 }
+// then [N][8H] f64 solutions, [N] i32 DM_BUCKET flags, and (256-aligned) the front DP's LP
+// cost-to-go rows [N][H + 1][64] (x, v)
+__host__ __device__ inline size_t w_region_offset(int N, int H) {
+    return (par_region_bytes(N, H) + (size_t)N * 8 * H * 8 + (size_t)N * sizeof(int) + 255) / 256 * 256;
+}
+__host__ __device__ inline size_t w_region_bytes(int N, int H) { return (size_t)N * (H + 1) * 64 * 16; }
 
 struct DirectLayout {
     int draw, oat, ghi, price, cA, cC, cq, sc, t2, bx0, bp1, bp2, lab, rmin, tail;
@@ -2089,12 +2097,44 @@ struct FrontBufs {
     const double *cA, *cC, *cq;          // [H] chain coefficients and duty costs
     double* x;                           // [8H] stage-slot solution (writes slots sx, sv)
     uint16_t* par;                       // [H][NB_CAP] global
+    double2* wg;                         // [H + 1][WAVE] global: LP cost-to-go W_j as points (x, v),
+                                         //   +inf padded; nullptr = no bound pruning
+    double *wlx, *wlv, *wls;             // [WAVE] LDS: the current stage's W (points, slopes)
 };
 
 // 1 / w to about 1 ulp: v_rcp_f64 and one Newton step (no IEEE division sequence)
 DEV double rcp_nr(double w) {
     double r = __builtin_amdgcn_rcp(w);
     return fma(fma(-w, r, 1.0), r, r);
+}
+
+// W, a convex piecewise-linear function, as m <= 64 points (x_i, v_i), one per lane (+inf past
+// m), ascending in x.  Value at a uniform point p inside [x_0, x_{m-1}] (v_readlane of the
+// segment found by a ballot).
+DEV double pl_eval(double wx, double wv, int m, double p) {
+    const int cnt = __popcll(__ballot(wx <= p));
+    const int i = min(max(cnt - 1, 0), m - 2);
+    const double x0 = read_lane(wx, i), x1 = read_lane(wx, i + 1);
+    const double v0 = read_lane(wv, i), v1 = read_lane(wv, i + 1);
+    const double w = x1 - x0;
+    return w > 0.0 ? fma((p - x0) * rcp_nr(w), v1 - v0, v0) : fmin(v0, v1);
+}
+// the lanes' points of one W into the LDS table (points, slopes to the next point)
+DEV void w_to_lds(const FrontBufs& B, int lane, double wx, double wv) {
+    const double nx = __shfl_down(wx, 1), nv = __shfl_down(wv, 1);
+    const double s = (lane < WAVE - 1 && nx < INFINITY && nx > wx) ? (nv - wv) * rcp_nr(nx - wx) : 0.0;
+    B.wlx[lane] = wx;
+    B.wlv[lane] = wv;
+    B.wls[lane] = s;
+}
+// W(x) at a per-lane point from the LDS table: binary search, then the segment's line (its linear
+// extension outside [x_0, x_{m-1}], where the integer programme has no schedule anyway)
+DEV double w_eval(const FrontBufs& B, double x) {
+    int i = 0;
+#pragma unroll
+    for (int st = WAVE / 2; st > 0; st >>= 1)
+        if (B.wlx[i + st] <= x) i += st;
+    return fma(x - B.wlx[i], B.wls[i], B.wlv[i]);
 }
 // inclusive scan over the 64 lanes with identity id (lanes shifted in from outside a row
 // keep id: bound_ctrl off), rows combined through v_readlane
@@ -2115,7 +2155,7 @@ DEV T dpp_iscan(T v, int lane, T id, Op op) {
 
 template <int SS>
 DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, double lo0, double hi0, double lo,
-                 double hi, int sx, int sv) {
+                 double hi, int sx, int sv, bool use_bound) {
     static_assert(SS > 0 && SS < 16, "duty count must be a compile-time constant below 16");
     constexpr int NU = SS + 1;
     constexpr int BPL = NTB / WAVE;      // buckets per lane in the scan
@@ -2132,7 +2172,10 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     }
     pos = __any(pos);
     neg = __any(neg);
-    if (pos && neg) return -1;
+    // the key orientation needs duty prices of one sign; otherwise (or on a feasible set narrower
+    // than a duty step, whose hull may hold unreachable states) the DP runs without dominance,
+    // on the bound alone (below), or falls back
+    bool nodom = pos && neg;
     const double dx = ((g > 0.0) != neg) ? 1.0 : -1.0;
     // (b) feasible-set hulls F_H .. F_1 (every lane computes, lane 0 stores).  Stored as 32-bit
     //     fixed point over [hb, hb + 2^32 hs], a range past every stage box and its tolerance
@@ -2164,8 +2207,107 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             if (lane == 0) { B.flo[k] = enc_lo(l); B.fhi[k] = enc_hi(u); }
         }
         if (empty) return 0;
-        if (narrow) return -1;
+        nodom = nodom || narrow;
     }
+    // (c) the LP cost-to-go W_j(x_j) (duties continuous in [0, S]) for j = H .. 1: convex,
+    //     piecewise linear, a lower bound of the integer cost-to-go.  From W_{j+1}: the duty's
+    //     cheapest use is full duty left of the minimiser of v + (q/g) x and none right of it,
+    //     so W_j is W_{j+1}'s point list with the minimiser doubled, the left part shifted by
+    //     -max(0, gS) at cost q S [g > 0], the right part by -min(0, gS) at q S [g < 0], mapped
+    //     through x = (y - C) / A and cut to x_j's box.  One point per lane, rows in B.wg.
+    //     More than 64 points, or a degenerate stage: no bound (exact all the same).
+    //     On by request (prices that change at most stages: fronts grow large without it) and
+    //     wherever dominance is off; the plain front DP is cheaper on piecewise-constant tariffs.
+    bool prune = B.wg != nullptr && (use_bound || nodom);
+    if (prune) {
+        double bl = H == 1 ? lo0 : lo, bh = H == 1 ? hi0 : hi;
+        bl -= tw(bl);
+        bh += tw(bh);
+        double wx = lane == 0 ? bl : lane == 1 ? bh : INFINITY, wv = lane < 2 ? 0.0 : INFINITY;
+        int m = 2;
+        B.wg[H * WAVE + lane] = make_double2(wx, wv);
+        for (int j = H - 1; j >= 1; --j) {
+            const double A = B.cA[j], C = B.cC[j], q = B.cq[j];
+            if (!(A > 0.0) || m + 1 > WAVE) { prune = false; break; }
+            const double zs = g * SS, cS = q * SS;
+            const double zlo = fmin(0.0, zs), zhi = fmax(0.0, zs);
+            const double cL = zs > 0.0 ? cS : 0.0, cR = zs > 0.0 ? 0.0 : cS;
+            const double F = lane < m ? fma(q * rcp_nr(g), wx, wv) : INFINITY;
+            const double Fm = dpp_reduce(F, [](double a, double b) { return fmin(a, b); });
+            const int js = __ffsll((long long)__ballot(F == Fm)) - 1;
+            const double px = __shfl_up(wx, 1), pv = __shfl_up(wv, 1);
+            const int m1 = m + 1;
+            const double iA = rcp_nr(A);
+            double nx = lane <= js ? wx - zhi : px - zlo;
+            double nv = lane <= js ? wv + cL : pv + cR;
+            nx = (nx - C) * iA;
+            if (lane >= m1) { nx = INFINITY; nv = INFINITY; }
+            double cl = j == 1 ? lo0 : lo, ch = j == 1 ? hi0 : hi;
+            cl -= tw(cl);
+            ch += tw(ch);
+            const double dl = fmax(cl, read_lane(nx, 0)), dh = fmin(ch, read_lane(nx, m1 - 1));
+            if (!(dl <= dh)) { prune = false; break; }
+            const double vdl = pl_eval(nx, nv, m1, dl), vdh = pl_eval(nx, nv, m1, dh);
+            const bool in = lane < m1 && nx > dl && nx < dh;
+            const unsigned long long bal = __ballot(in);
+            const int m2 = __popcll(bal) + 2;
+            if (m2 > WAVE) { prune = false; break; }
+            // compact through the LDS table (free here)
+            if (in) {
+                const int pos_ = 1 + __popcll(bal & ((1ull << lane) - 1ull));
+                B.wlx[pos_] = nx;
+                B.wlv[pos_] = nv;
+            }
+            if (lane == 0) {
+                B.wlx[0] = dl; B.wlv[0] = vdl;
+                B.wlx[m2 - 1] = dh; B.wlv[m2 - 1] = vdh;
+            }
+            __syncthreads();
+            wx = lane < m2 ? B.wlx[lane] : INFINITY;
+            wv = lane < m2 ? B.wlv[lane] : INFINITY;
+            m = m2;
+            __syncthreads();
+            B.wg[j * WAVE + lane] = make_double2(wx, wv);
+        }
+    }
+    // (d) an upper bound: the cost of one feasible schedule, greedy in q u + W_{k+1}(x') (the
+    //     labels' own arithmetic).  Children with cost + W > bound (+ a margin past rounding)
+    //     cannot lead to the optimum and are dropped.
+    double UBT = INFINITY;
+    if (prune) {
+        double qabs = 0.0;
+        for (int k = lane; k < H; k += WAVE) qabs += fabs(B.cq[k]) * SS;
+        qabs = dpp_sum(qabs);
+        double gx = x0, ub = 0.0;
+        bool gok = true;
+        double2 cur = B.wg[WAVE + lane];
+        for (int k = 0; k < H && gok; ++k) {
+            double2 nxt = k + 2 <= H ? B.wg[(k + 2) * WAVE + lane] : make_double2(INFINITY, INFINITY);
+            w_to_lds(B, lane, cur.x, cur.y);
+            __syncthreads();
+            const double A = B.cA[k], C = B.cC[k], q = B.cq[k];
+            double bl = k == 0 ? lo0 : lo, bh = k == 0 ? hi0 : hi;
+            bl -= tw(bl);
+            bh += tw(bh);
+            if (k + 1 < H) {
+                bl = fmax(bl, fma((double)B.flo[k + 1], hs, hb));
+                bh = fmin(bh, fma((double)B.fhi[k + 1], hs, hb));
+            }
+            const double xc = fma(A, gx, fma(g, (double)lane, C));
+            double val = INFINITY;
+            if (lane <= SS && xc >= bl && xc <= bh) val = (double)lane * q + w_eval(B, xc);
+            const double vm = dpp_reduce(val, [](double a, double b) { return fmin(a, b); });
+            if (!(vm < INFINITY)) { gok = false; break; }
+            const int bu = __ffsll((long long)__ballot(val == vm)) - 1;
+            gx = read_lane(xc, bu);
+            ub = fma(q, (double)bu, ub);
+            cur = nxt;
+            __syncthreads();
+        }
+        if (gok) UBT = ub + TOL_P * (1.0 + fabs(ub) + qabs);
+        else prune = false;
+    }
+    if (nodom && !prune) return nodom && (pos && neg) ? -1 : -2;
     // the front stores each label's exact STATE x (not its key dx * x) and cost
     double2* fa = B.fa;
     double2* fb = B.fb;
@@ -2174,6 +2316,12 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     double xmin = x0, xmax = x0, cmin = 0.0, cmax = 0.0;    // state / cost range of the front
     const unsigned long long below = (1ull << lane) - 1ull;  // lanes < this one
     for (int b = lane; b < NTB; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
+    // W_{k+1} of the stage in the LDS table, W_{k+2} in flight
+    double2 wnext = make_double2(INFINITY, INFINITY);
+    if (prune) {
+        w_to_lds(B, lane, B.wg[WAVE + lane].x, B.wg[WAVE + lane].y);
+        if (H >= 2) wnext = B.wg[2 * WAVE + lane];
+    }
     __syncthreads();
     for (int k = 0; k < H; ++k) {
         const double A = B.cA[k], C = B.cC[k], q = B.cq[k];
@@ -2211,12 +2359,12 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         // 1. per key bucket the cheapest child (largest key among equally cheap ones), per
         //    cost bucket the largest-key child (cheapest among equal keys), both as
         //    understated bounds (cost up, key down), by 64-bit LDS atomics
-        for (int c = lane; c < nc; c += WAVE) {
+        for (int c = lane; c < nc && !nodom; c += WAVE) {
             const int i = c / NU, u = c - i * NU;
             const double2 Li = fa[i];
             const double xc = fma(A, Li.x, fma(g, (double)u, C));
-            if (xc >= bl && xc <= bh) {
-                const double cc = fma(q, (double)u, Li.y);
+            const double cc = fma(q, (double)u, Li.y);
+            if (xc >= bl && xc <= bh && (!prune || cc + w_eval(B, xc) <= UBT)) {
                 const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
                 const unsigned cu = vc + 2u, kd = dn(vk);
                 atomicMin(&B.kb[min(NTB - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
@@ -2227,7 +2375,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         // 2. mh[b] = min cost over the key buckets above b (lane l holds key chunk 63 - l:
         //    "above" = lower lanes, an exclusive prefix-min); kl[b] = max key over the cost
         //    buckets below b (lane l holds cost chunk l: an exclusive prefix-max)
-        {
+        if (!nodom) {
             const int c0 = (WAVE - 1 - lane) * BPL, d0 = lane * BPL;
             unsigned bm[BPL], bk[BPL];
             unsigned lm = ~0u, lk = 0u;
@@ -2273,7 +2421,8 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             const double cc = fma(q, (double)u, Li.y);
             const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
             bool keep = have && xc >= bl && xc <= bh;
-            if (keep) {
+            if (keep && prune) keep = cc + w_eval(B, xc) <= UBT;
+            if (keep && !nodom) {
                 const int kbk = min(NTB - 1, (int)(vk >> 23)), cbk = min(NTB - 1, (int)(vc >> 23));
                 const unsigned ku = vk + 2u, cd = dn(vc);
                 const unsigned long long ky = B.kb[kbk], cy = B.cb[cbk];
@@ -2288,15 +2437,19 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             const unsigned long long bal = __ballot(keep);
             const int slot = nn + __popcll(bal & below);
             nn += __popcll(bal);
-            if (keep && slot < NF) {
+            if (keep && slot < (prune ? NF_BOUND : NF)) {
                 fb[slot] = make_double2(xc, cc);
                 B.par[k * NB_CAP + slot] = (uint16_t)(i | (u << 12));
                 kmn = umin(kmn, vk); kmx = umax(kmx, vk);
                 cmn = umin(cmn, vc); cmx = umax(cmx, vc);
             }
         }
+#ifdef DRAGG_FRONT_STATS
+        if (lane == 0) B.x[k * 8 + S_PAD] += (double)nn * (B.x[sx] == -12345.0 ? 1.0 : 1.0) * (sx == S_T ? 1.0 : 1e4) +
+                                             (k == 0 ? (prune ? 1e8 : 0.0) * (sx == S_T ? 1.0 : 2.0) : 0.0);
+#endif
         if (nn == 0) return 0;                       // no child left inside the feasible set
-        if (nn > NF) return -1;                      // front overflow
+        if (nn > (prune ? NF_BOUND : NF)) return -3;  // front overflow
         // the next stage's state and cost ranges from the survivors' positions: the exact
         // position V of a value lies in [v - 1, v + 2], widened past the back-conversion's
         // rounding
@@ -2314,7 +2467,11 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             cmin = c1 - tw(c1);
             cmax = c2 + tw(c2);
         }
-        for (int b = lane; b < NTB; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
+        for (int b = lane; b < NTB && !nodom; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
+        if (prune && k + 1 < H) {
+            w_to_lds(B, lane, wnext.x, wnext.y);
+            if (k + 3 <= H) wnext = B.wg[(k + 3) * WAVE + lane];
+        }
         __syncthreads();
         double2* tmp = fa; fa = fb; fb = tmp;
         n = nn;
@@ -2364,6 +2521,7 @@ DEV bool round_duties(const Home& h, const Lds& L, int lane, uint16_t* par) {
     B.flo = reinterpret_cast<unsigned*>(f); f += (H + 2) / 2;
     B.fhi = reinterpret_cast<unsigned*>(f); f += (H + 2) / 2;
     B.cA = cA; B.cC = cC; B.cq = cq; B.x = L.x; B.par = par;
+    B.wg = nullptr; B.wlx = B.wlv = B.wls = nullptr;     // no bound pruning on this path
     const bool front = h.S == 6 && par != nullptr && (f - L.Lf) <= 128 * H;
     for (int k = lane; k < H; k += WAVE) {
         cA[k] = h.aT;
@@ -2577,6 +2735,11 @@ __global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_ker
         // chain 0: indoor air (mpc_calc.py:314-317), u = duty of the season's mode (:303-309);
         // chain 1: water heater given T (mpc_calc.py:330-332).  One DP instantiation for both.
         bool ok = true;
+        // prices that change at more than a quarter of the stages (RL reward prices; a tariff
+        // changes a few times a day): the front DP runs with its LP bound
+        int changes = 0;
+        for (int k = lane; k < H; k += NT) changes += (k > 0 && D.price[k] != D.price[k - 1]) ? 1 : 0;
+        const bool use_bound = dpp_isum(changes) * 4 > H;
         for (int chain = 0; chain < 2 && ok; ++chain) {
             reload_home(h, a, home, saved);
             twlo0 = saved[6]; twhi0 = saved[7];
@@ -2605,8 +2768,12 @@ __global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_ker
             // prices, a feasible set narrower than one duty step, front overflow, S != 6)
             int r = -1;
             if (h.S == 6) {
-                const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par};
-                r = dp_front<6>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv);
+                double* const wl = reinterpret_cast<double*>(D.rmin + NF_BOUND);   // past the front
+                double2* const wg = reinterpret_cast<double2*>(reinterpret_cast<char*>(a.p.workspace) +
+                                                               w_region_offset(N, H)) + (size_t)home * (H + 1) * WAVE;
+                const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
+                                   wg, wl, wl + WAVE, wl + 2 * WAVE};
+                r = dp_front<6>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
             }
             if (r >= 0) {
                 ok = r == 1;
@@ -2614,7 +2781,7 @@ __global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_ker
                 if (lane == 0) defer[home] = 1;
                 return;
             } else {
-                int_path |= 1 << chain;
+                int_path |= (1 << chain) | ((-r) << (4 + 4 * chain));   // chain bit + reason
                 ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
                               : dp_thermal<0>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
             }
@@ -2687,12 +2854,10 @@ __global__ void noise_kernel(int N, int H, uint64_t seed, int off, int stride, i
 bool direct_mode(const dragg_mpc_dims* d) { return d->int_mode == DRAGG_INT_ROUND; }
 
 size_t workspace_bytes(const dragg_mpc_dims* d) {
-    // direct: [N][H][NB_CAP] u16 back-pointers, [N][8H] f64 solutions, [N] i32 DM_BUCKET flags;
-    // round_lp: the back-pointers of its front DP
+    // direct: [N][H][NB_CAP] u16 back-pointers, [N][8H] f64 solutions, [N] i32 DM_BUCKET flags,
+    // [N][H+1][64] LP cost-to-go rows; round_lp: the back-pointers of its front DP
     if (d->int_mode == DRAGG_INT_ROUND_LP) return par_region_bytes(d->n_homes, d->horizon);
-    return direct_mode(d) ? par_region_bytes(d->n_homes, d->horizon) + (size_t)d->n_homes * 8 * d->horizon * 8 +
-                                (size_t)d->n_homes * sizeof(int)
-                          : 0;
+    return direct_mode(d) ? w_region_offset(d->n_homes, d->horizon) + w_region_bytes(d->n_homes, d->horizon) : 0;
 }
 
 size_t kernel_lds_bytes(const dragg_mpc_dims* d) {

@@ -155,8 +155,9 @@ typedef struct dragg_mpc_out {
     int32_t* int_path;          /* optional [N] integer-DP path (int_mode round): 0 = the
                                    exact front DP solved both thermal chains; bit 0 / bit 1
                                    = the indoor-air / tank chain used the bucketed
-                                   approximation (mixed-sign prices, a feasible set narrower
-                                   than one duty step, front overflow)                   */
+                                   approximation; bits 4-7 / 8-11 its reason: 1 mixed-sign
+                                   prices, 2 a feasible set narrower than one duty step,
+                                   3 front overflow                                      */
 } dragg_mpc_out;
 
 /* solver phases timed into dragg_mpc_out.cycles (diagnostic; NULL = not stamped) */
