@@ -1,14 +1,18 @@
 // mpc_kernel.hip -- batched per-home HEMS MPC for MI355X (gfx950, CDNA4).
 //
-// One 64-lane workgroup (one wavefront) owns one home for one timestep.  The home's
-// MILP from dragg/mpc_calc.py:291-446 is rebuilt on device in a stage-ordered chain
-// form (8 variable slots and 3 dynamics rows per stage), the LP relaxation is solved
-// by an OSQP-style ADMM whose block-tridiagonal KKT factor (8x8 blocks, lane (i,j) of
-// the wave owns entry (i,j)) lives in LDS, and every `check_every` iterations an exact
-// basis polish recovers the vertex and certifies it (primal feasibility + reduced-cost
-// signs).  The integer duty cycles are then rounded feasibly, and the reference's
-// result extraction / fallback thermostat (mpc_calc.py:476-596) writes the per-home
-// hash arrays in place.  See DESIGN.md for the formulation and roofline.
+// One 64-lane workgroup (one wavefront) owns one home for one timestep.  The home's MILP
+// (dragg/mpc_calc.py:291-446) is separable: the default path (int_mode round,
+// mpc_direct_kernel) solves it exactly -- the two thermal integer chains by a forward
+// Pareto-front DP (dp_front: labels (state, cost) with dominance filters on two bucket grids,
+// optionally pruned by an LP cost-to-go bound), the battery LP by an exact convex
+// piecewise-linear DP (battery_lp), PV curtailment in closed form -- in a first launch
+// (DM_FRONT); homes whose chains leave the front DP's scope (front overflow, mixed-sign prices
+// without a usable bound) are finished by a second launch (DM_BUCKET) with the bucketed DP.
+// int_mode relax / round_lp (mpc_home_kernel) solve the LP relaxation by an OSQP-style ADMM
+// whose block-tridiagonal KKT factor lives in LDS, with an exact basis polish every
+// `check_every` iterations, then (round_lp) the same integer DP.  The reference's result
+// extraction / fallback thermostat (mpc_calc.py:476-596) writes the per-home hash arrays in
+// place.  See DESIGN.md for the formulation and roofline.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>

@@ -10,7 +10,11 @@
  *     water_draws             mpc_calc.py:193     (computed on device from draw_hourly)
  *     set_environmental_vars  mpc_calc.py:206     (slices of oat/ghi/tou + reward price)
  *     add_*_constraints       mpc_calc.py:291-432 (built on device, never materialised)
- *     solve_mpc (GLPK_MI)     mpc_calc.py:434     (batched banded-KKT ADMM + exact polish)
+ *     solve_mpc (GLPK_MI)     mpc_calc.py:434     (int_mode round, default: the MILP solved
+ *                                                  exactly -- thermal chains by an exact
+ *                                                  Pareto-front DP, battery by an exact
+ *                                                  piecewise-linear DP; relax / round_lp:
+ *                                                  banded-KKT ADMM + exact vertex polish)
  *     cleanup_and_finish      mpc_calc.py:476     (success extraction / fallback thermostat)
  *     redis_write_optimal_vals mpc_calc.py:100    (hash arrays updated in place)
  *   manage_home + ProcessPool aggregator.py:723   one launch over all homes of a timestep
@@ -86,11 +90,11 @@ enum dragg_val {
 
 /* per-home status written by a step (status[N]) */
 enum dragg_status {
-    DRAGG_ST_OPTIMAL = 0,          /* LP optimal (exact vertex) and integer rounding succeeded  */
+    DRAGG_ST_OPTIMAL = 0,          /* solved: the MILP optimum (round) / LP vertex (relax)      */
     DRAGG_ST_INFEASIBLE = 1,       /* proven infeasible by interval presolve                   */
     DRAGG_ST_INFEASIBLE_CERT = 2,  /* ADMM primal-infeasibility certificate                     */
     DRAGG_ST_MAX_ITER = 3,         /* no verified vertex within max_iter                         */
-    DRAGG_ST_ROUND_FAIL = 4,       /* relaxation optimal, no integer duty schedule found         */
+    DRAGG_ST_ROUND_FAIL = 4,       /* boxes pass presolve, but no integer duty schedule exists  */
     DRAGG_ST_ERR_PARSE = 5,        /* fallback's float(str[0]) would raise (mpc_calc.py:537)     */
     DRAGG_ST_ERR_MISSING = 6       /* hash field missing at t>0 (KeyError, mpc_calc.py:280-289)  */
 };
@@ -101,7 +105,7 @@ enum dragg_mpc_error {
 
 /* integer handling of the duty-cycle variables (mpc_calc.py:171-173) */
 enum dragg_int_mode {
-    DRAGG_INT_ROUND = 0,    /* MILP: thermal integer DP + exact battery LP (default)   */
+    DRAGG_INT_ROUND = 0,    /* MILP, exact: thermal front DP + battery LP DP (default) */
     DRAGG_INT_RELAX = 1,    /* LP relaxation (ADMM + exact vertex polish)             */
     DRAGG_INT_ROUND_LP = 2  /* LP relaxation for status/battery, then the integer DP  */
 };

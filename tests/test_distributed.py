@@ -1,7 +1,7 @@
 """Multi-rank glue of the device-resident driver on CPU with gloo (world size 2).
 
 The solver is replaced by a stand-in batch (the HIP solver needs a GPU); what is tested is
-the sharding (contiguous blocks of the global community order, keyed by the global index)
+the sharding (strided shards: rank r holds homes r, r + world, ..., keyed by the global index)
 and the per-step all-reduce of [agg_load, forecast_load, agg_cost] (aggregator.py:751-753).
 """
 import os
