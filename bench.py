@@ -22,6 +22,7 @@ only): the repo's CPU restatement of the reference solve (oracle/, HiGHS MILP in
 GLPK_MI) timed on this host's cores on a bounded sample of the same workload.
 """
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -146,9 +147,65 @@ def measured_pmc(workload_key):
     return {}, None
 
 
-# VALU issue peak: a wave64 VALU instruction (fp64 FMA included) occupies its SIMD 4 cycles;
-# 256 CUs x 4 SIMDs at 2.4 GHz (MI355X_MICROARCH.md) -> wave-instructions per second
-VALU_PEAK = 256 * 4 * 2.4e9 / 4
+# Issue model of the VALU bound (MI355X_MICROARCH.md "Wave scheduling": a SIMD-32 issues a
+# wave64 VALU instruction over 2 cycles; fp64 add/mul/fma run at half the fp32 rate (78.6 vs
+# 157.3 TFLOPS): 4 cycles; fp64 transcendental (v_rcp_f64) a quarter of that: 8).  The rest
+# (int32/int64, conversions, moves, compares, lane ops) is priced at 2 cycles.  Peak: 256 CUs x
+# 4 SIMDs x 2.4 GHz SIMD-cycles per second.
+N_SIMD, CLOCK = 256 * 4, 2.4e9
+LDS_PEAK_TBS = 150.0      # ds_read_b64/b128 with every CU streaming (MI355X_MICROARCH.md, LDS)
+
+
+def valu_cycles(sq):
+    f64 = sq.get("SQ_INSTS_VALU_ADD_F64", 0) + sq.get("SQ_INSTS_VALU_MUL_F64", 0) + sq.get("SQ_INSTS_VALU_FMA_F64", 0)
+    trans = sq.get("SQ_INSTS_VALU_TRANS_F64", 0)
+    return 2.0 * (sq["SQ_INSTS_VALU"] - f64 - trans) + 4.0 * f64 + 8.0 * trans
+
+
+def extra_rooflines(pmc, kern_ms, lds_bytes_per_home, src):
+    """The bounds that do limit the kernel, from the committed PMC passes of
+    this workload (per solver step) and the step's kernel time measured in this run."""
+    sq = pmc.get("sq_per_launch", {})
+    if "SQ_INSTS_VALU" not in sq:
+        return {}
+    ks = kern_ms * 1e-3
+    out = {}
+    if "SQ_INSTS_VALU_FMA_F64" in sq:
+        cyc = valu_cycles(sq)
+        out["roofline_valu"] = {
+            "bound": "valu-issue", "achieved": cyc / ks / 1e12, "peak": N_SIMD * CLOCK / 1e12,
+            "unit": "T SIMD-cycles/s", "frac": cyc / ks / (N_SIMD * CLOCK),
+            "valu_per_launch": sq["SQ_INSTS_VALU"],
+            "fp64_valu_per_launch": sum(sq.get(f"SQ_INSTS_VALU_{c}_F64", 0) for c in ("ADD", "MUL", "FMA", "TRANS")),
+            "model": "2 cycles per wave64 VALU instruction, 4 per fp64 add/mul/fma, 8 per fp64 transcendental",
+            "source": src}
+    if "SQ_ACTIVE_INST_VALU" in sq and "SQ_WAVE_CYCLES" in sq:
+        out["valu_busy_per_wave"] = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
+    if "SQ_INSTS_LDS" in sq:
+        # upper estimate of LDS bytes: every LDS instruction moving 8 B for all 64 lanes
+        b = sq["SQ_INSTS_LDS"] * 64 * 8
+        out["roofline_lds"] = {
+            "bound": "lds", "achieved": b / ks / 1e12, "peak": LDS_PEAK_TBS, "unit": "TB/s",
+            "frac": b / ks / 1e12 / LDS_PEAK_TBS, "lds_instr_per_launch": sq["SQ_INSTS_LDS"],
+            "bank_conflict_share": (sq["SQ_LDS_BANK_CONFLICT"] / sq["SQ_LDS_IDX_ACTIVE"]
+                                    if sq.get("SQ_LDS_IDX_ACTIVE") else None),
+            "assumption": "8 B x 64 lanes per LDS instruction (an upper estimate; most are b64)", "source": src}
+    homes_per_cu = (160 * 1024) // max(1, lds_bytes_per_home)
+    out["occupancy"] = {"lds_bytes_per_home": lds_bytes_per_home, "homes_per_cu_lds": homes_per_cu,
+                        "waves_per_simd": min(homes_per_cu / 4.0, 2.0),
+                        "limit": "LDS (one 64-lane workgroup per home) and 164 VGPRs: 2 waves per SIMD",
+                        "wait_share": (sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"] if "SQ_WAIT_ANY" in sq else None),
+                        "issue_share": (sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"]
+                                        if "SQ_ACTIVE_INST_ANY" in sq else None)}
+    fs = pmc.get("front_stats")
+    if fs:
+        out["dp_work"] = {"unit": "G label relaxations/s", "achieved": fs["children_per_launch"] / ks / 1e9,
+                          "children_per_launch": fs["children_per_launch"],
+                          "front_mean": [fs["front_mean_T"], fs["front_mean_W"]],
+                          "definition": "one label relaxation = one child (parent label, duty) of a front DP stage: "
+                                        "state and cost update, box test, bucket positions, dominance tests",
+                          "source": src}
+    return out
 
 
 def traffic_key(n_total, H, dt, month, int_mode, world):
@@ -258,7 +315,6 @@ def main():
         achieved = bytes_per_launch(agg.batch, success) / (kern_ms * 1e-3) / 1e9
         pmc, traffic_src = measured_pmc(traffic_key(n_total, H, dt, args.month, args.int_mode, world))
         traffic = pmc.get("bytes_per_launch")
-        valu = pmc.get("sq_per_launch", {}).get("SQ_INSTS_VALU")
         out = {
             "metric": "home-MPC solves/sec (homes x steps)", "value": value, "unit": "solves/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -274,20 +330,16 @@ def main():
                          "frac": achieved / 8000.0,
                          "traffic": (traffic / (kern_ms * 1e-3) / 1e9) if traffic else None,
                          "traffic_bytes_per_launch": traffic, "traffic_source": traffic_src,
-                         "kernel": f"mpc_{'direct' if args.int_mode == 'round' else 'home'}_kernel",
+                         "kernel": (f"mpc_direct_kernel (DM_FRONT + DM_BUCKET launches of a step)"
+                                    if args.int_mode == "round" else "mpc_home_kernel"),
                          "kernel_ms": kern_ms},
-            # the bound that does limit the kernel: VALU issue.  Achieved =
-            # VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU, committed pass of this
-            # workload) / the launch time measured here
-            "roofline_valu": ({"bound": "valu-issue", "achieved": valu / (kern_ms * 1e-3) / 1e9,
-                               "peak": VALU_PEAK / 1e9, "unit": "G wave-instr/s",
-                               "frac": valu / (kern_ms * 1e-3) / VALU_PEAK, "valu_per_launch": valu,
-                               "source": traffic_src} if valu else None),
             "cpu_baseline": cpu,
             "status_counts": stat_counts,
             # RL: the headline counts the rollout re-solves too; the committed steps alone:
             "committed_solves_per_s": n_total * args.steps / elapsed,
         }
+        out.update(extra_rooflines(pmc, kern_ms, agg.batch.lib.dragg_mpc_lds_bytes(ctypes.byref(agg.batch.dims)),
+                                   traffic_src))
         print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

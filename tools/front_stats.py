@@ -12,7 +12,7 @@ from dragg_amd.mpc import MPCBatch                                   # noqa: E40
 from dragg_amd.community import synthetic_homes, synthetic_weather   # noqa: E402
 
 N, HH, MONTH = (int(x) for x in sys.argv[1:4])
-rl = len(sys.argv) > 4
+rl = "rl" in sys.argv[4:]
 dt = 4
 days = 3
 homes = synthetic_homes(N, seed=12, days=days, dt=dt, horizon_hours=HH)
@@ -31,6 +31,18 @@ v[:, 0] -= pr * 1e8
 nW = np.floor(v / 1e4)
 nT = v - nW * 1e4
 ok = st == 0
+if "--json" in sys.argv:
+    import json
+    # children evaluated per stage = 7 x the previous stage's front (1 label before stage 0)
+    prevT = np.concatenate([np.ones((N, 1)), nT[:, :-1]], axis=1)
+    prevW = np.concatenate([np.ones((N, 1)), nW[:, :-1]], axis=1)
+    kids = 7.0 * (prevT[ok].sum() + prevW[ok].sum())
+    json.dump({"workload": f"{N} homes, H={H}, month {MONTH}, rl={rl}, one step (t = 0)",
+               "front_mean_T": float(nT[ok].mean()), "front_mean_W": float(nW[ok].mean()),
+               "front_max": float(max(nT[ok].max(), nW[ok].max())),
+               "children_per_launch": float(kids) * N / max(1, int(ok.sum())),
+               "note": "label relaxations (children) per launch, scaled from the optimal homes to all homes"},
+              open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
 print(f"N={N} H={H} rl={rl}: optimal {ok.sum()}; prune flag (1 T, 2 W, 3 both) counts {np.unique(pr[ok], return_counts=True)}")
 for name, a in (("T", nT[ok]), ("W", nW[ok])):
     mx = a.max(axis=1)

@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/prof
 mkdir -p $OUT
-ARGS=${@:-"--homes 10000 --horizon-hours 12 --month 7 --steps 6 --warmup 1 --cpu-seconds 0"}
+ARGS=${@:-"--cpu-seconds 0"}          # the bench's default workload (96 steps), CPU leg skipped
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_available.txt 2>&1 || true
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || exit 1
 pass() {
@@ -15,6 +15,11 @@ pass() {
 }
 pass sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS || exit 1
 pass sq2 SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH || exit 1
+pass sq3 SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT || exit 1
+pass sq4 SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT SQ_INST_CYCLES_SALU || exit 1
 pass fetch FETCH_SIZE || exit 1
 pass write WRITE_SIZE || exit 1
+if [ -f varlib/stats.so ]; then
+  DRAGG_LIB=varlib/stats.so timeout -k 10 200 python tools/front_stats.py 10000 12 7 --json $OUT/front_stats.json > $OUT/front_stats.log 2>&1 || exit 1
+fi
 echo done

@@ -16,11 +16,17 @@ sys.path.insert(0, ROOT)
 
 
 def per_dispatch(path, counter, kernel_sub):
-    vals = {}
+    """Per solver STEP: the step's launches (DM_FRONT and the DM_BUCKET second launch, both named
+    mpc_direct_kernel) summed, averaged over the steps (= the DM_FRONT dispatches) -- the unit
+    bench.py times with its events around run_iteration."""
+    vals, first = {}, set()
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter and kernel_sub in r["Kernel_Name"]:
             vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    return sum(vals.values()) / max(1, len(vals)), len(vals)
+            if "<false, 0>" in r["Kernel_Name"] or "<true, 0>" in r["Kernel_Name"] or "direct" not in kernel_sub:
+                first.add(r["Dispatch_Id"])
+    steps = max(1, len(first) or len(vals))
+    return sum(vals.values()) / steps, steps
 
 
 def main():
@@ -44,7 +50,7 @@ def main():
            "bytes_per_launch": (2.0 * fetch + write) * 1024.0,
            "formula": "(2 x FETCH_SIZE + WRITE_SIZE) x 1024, rocprofv3 --pmc, separate passes"}
     sq = {}
-    for p in ("sq1", "sq2"):
+    for p in ("sq1", "sq2", "sq3", "sq4"):
         f = os.path.join(a.prof, p, f"{p}_counter_collection.csv")
         if not os.path.exists(f):
             continue
@@ -52,6 +58,10 @@ def main():
             sq[c] = per_dispatch(f, c, a.kernel)[0]
     if sq:
         out["sq_per_launch"] = sq
+    fs = os.path.join(a.prof, "front_stats.json")
+    if os.path.exists(fs):
+        with open(fs) as f:
+            out["front_stats"] = json.load(f)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
