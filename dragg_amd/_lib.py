@@ -31,6 +31,10 @@ NVAL = len(VAL_KEYS)
 K = {k: i for i, k in enumerate(VAL_KEYS)}
 
 ST_OPTIMAL, ST_INFEASIBLE, ST_INFEASIBLE_CERT, ST_MAX_ITER, ST_ROUND_FAIL, ST_ERR_PARSE, ST_ERR_MISSING = range(7)
+# int_path bits (dragg_mi355x.h): 0-11 = a chain left the exact front DP (chain bits + reasons);
+# PATH_SECOND = the home was solved by the second launch (exact unless bits 0-11 are set)
+PATH_APPROX_MASK = 0xFFF
+PATH_SECOND = 1 << 12
 STATUS_NAMES = ["optimal", "infeasible", "infeasible_cert", "max_iter", "round_fail", "err_parse",
                 "err_missing"]
 

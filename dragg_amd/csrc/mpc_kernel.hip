@@ -34,6 +34,8 @@ constexpr int NBND = 8;              // box-boundary buckets per stage (dp_zspac
 constexpr int NF = NB_CAP;              // front capacity (labels) of dp_front
 constexpr int NF_BOUND = 240;           // ... when the LP bound is on: its W table follows the front
 static_assert((NB_CAP + 8 - NF_BOUND) * 16 >= 3 * 64 * 8, "the W table lives in rmin past the front");
+constexpr int NF_BIG = 2048;            // front capacity of the second launch's exact pass
+constexpr int SECOND_SLOTS = 512;       // blocks of the persistent second launch (2 per CU)
 constexpr int NTB = 256;             // key buckets and cost buckets per stage (dp_front)
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
 
@@ -1016,9 +1018,10 @@ DEV bool dp_chain(const Home& h, const Lds& L, const DpChain& c, int lane) {
     return true;
 }
 
-template <int SS>
+template <int SS, int CAP = NF, int CAPB = NF_BOUND, int PS = NB_CAP>
 DEV int dp_front(const struct FrontBufs& B, int H, int lane, double g, double x0, double lo0, double hi0, double lo,
-                 double hi, int sx, int sv, bool use_bound = false);
+                 double hi, int sx, int sv, bool use_bound = false, double ub_ext = INFINITY,
+                 double* best_out = nullptr);
 
 // int_mode round_lp: the integer duties after the relaxation, by the exact front DP (the
 // default path's, dp_front) with its buffers in the KKT-factor LDS the ADMM no longer needs
@@ -1394,6 +1397,7 @@ struct LdsD {
     int16_t *tarr, *rsrc;               // [NB_CAP], [NB_CAP+8] source keys, source of rmin
     double *sgS, *sgL;                  // battery segments [2][seg_cap], in lab / rmin (the
                                         //   battery LP runs after the thermal DPs)
+    double* wl;                         // [3][WAVE] dp_front's W table (points, values, slopes)
     uint16_t* par;                      // [H][NB_CAP] DP back-pointers (global workspace)
 };
 
@@ -1413,12 +1417,19 @@ __host__ __device__ inline bool direct_fits(int H) { return seg_cap(H) <= NB_CAP
 __host__ __device__ inline size_t par_region_bytes(int N, int H) {
     return ((size_t)N * H * NB_CAP * sizeof(uint16_t) + 255) / 256 * 256;
 }
-// then [N][8H] f64 solutions, [N] i32 DM_BUCKET flags, and (256-aligned) the front DP's LP
-// cost-to-go rows [N][H + 1][64] (x, v)
+// then [N][8H] f64 solutions, the list of homes the hot launch defers to the second one
+// ([N] i32 + its length), (256-aligned) the front DP's LP cost-to-go rows [N][H + 1][64] (x, v),
+// and (256-aligned) the second launch's back-pointer rows [SECOND_SLOTS][H][NF_BIG] u16, one
+// block of that persistent launch per slot
+__host__ __device__ inline size_t defer_offset(int N, int H) { return par_region_bytes(N, H) + (size_t)N * 8 * H * 8; }
 __host__ __device__ inline size_t w_region_offset(int N, int H) {
-    return (par_region_bytes(N, H) + (size_t)N * 8 * H * 8 + (size_t)N * sizeof(int) + 255) / 256 * 256;
+    return (defer_offset(N, H) + (size_t)(N + 1) * sizeof(int) + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t w_region_bytes(int N, int H) { return (size_t)N * (H + 1) * 64 * 16; }
+__host__ __device__ inline size_t big_region_offset(int N, int H) {
+    return (w_region_offset(N, H) + w_region_bytes(N, H) + 255) / 256 * 256;
+}
+__host__ __device__ inline size_t big_region_bytes(int H) { return (size_t)SECOND_SLOTS * H * NF_BIG * sizeof(uint16_t); }
 
 struct DirectLayout {
     int draw, oat, ghi, price, cA, cC, cq, sc, t2, bx0, bp1, bp2, lab, rmin, tail;
@@ -1470,6 +1481,30 @@ __host__ __device__ inline DirectLayout direct_layout(int H, int S) {
 
 __host__ __device__ inline int direct_lds_bytes(int H, int S) { return direct_layout(H, S).bytes; }
 
+// The second launch: the direct layout, and over its DP arrays (from lab on; the bucketed DP
+// is done with them, its schedule is in the global solution array) the big exact pass's
+// fronts [NF_BIG], W table, bucket arrays and hull.
+struct BigLayout {
+    int fa, fb, wl, kb, cb, mh, kl, flo, fhi, bytes;
+};
+__host__ __device__ inline BigLayout big_layout(int H, int S) {
+    const DirectLayout d = direct_layout(H, S);
+    BigLayout o{};
+    int p = d.lab;
+    auto take = [&](int bytes, int align) { p = (p + align - 1) / align * align; const int r = p; p += bytes; return r; };
+    o.fa = take(16 * NF_BIG, 16);
+    o.fb = take(16 * NF_BIG, 16);
+    o.wl = take(8 * 3 * WAVE, 16);
+    o.kb = take(8 * NTB, 16);
+    o.cb = take(8 * NTB, 16);
+    o.mh = take(4 * NTB, 4);
+    o.kl = take(4 * NTB, 4);
+    o.flo = take(4 * (H + 1), 4);
+    o.fhi = take(4 * (H + 1), 4);
+    o.bytes = (max(p, d.bytes) + 15) / 16 * 16;
+    return o;
+}
+
 DEV LdsD carve_direct(double* smem, int H, int S) {
     const DirectLayout o = direct_layout(H, S);
     char* b = reinterpret_cast<char*>(smem);
@@ -1492,6 +1527,7 @@ DEV LdsD carve_direct(double* smem, int H, int S) {
     L.candp = reinterpret_cast<int*>(b + o.candp);
     L.tarr = reinterpret_cast<int16_t*>(b + o.tarr);
     L.rsrc = reinterpret_cast<int16_t*>(b + o.rsrc);
+    L.wl = reinterpret_cast<double*>(L.rmin + NF_BOUND);        // past the bounded front
     const int sc = seg_cap(H);
     L.sgS = reinterpret_cast<double*>(L.lab);
     L.sgL = reinterpret_cast<double*>(L.rmin);
@@ -2157,10 +2193,11 @@ DEV T dpp_iscan(T v, int lane, T id, Op op) {
     return row == 0 ? v : op(v, off);
 }
 
-template <int SS>
+template <int SS, int CAP, int CAPB, int PS>
 DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, double lo0, double hi0, double lo,
-                 double hi, int sx, int sv, bool use_bound) {
+                 double hi, int sx, int sv, bool use_bound, double ub_ext, double* best_out) {
     static_assert(SS > 0 && SS < 16, "duty count must be a compile-time constant below 16");
+    static_assert(CAP <= PS && CAPB <= PS && PS <= 4096, "back-pointer rows hold a 12-bit parent index");
     constexpr int NU = SS + 1;
     constexpr int BPL = NTB / WAVE;      // buckets per lane in the scan
     static_assert(NTB % WAVE == 0, "");
@@ -2309,9 +2346,12 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             __syncthreads();
         }
         if (gok) UBT = ub + TOL_P * (1.0 + fabs(ub) + qabs);
-        else prune = false;
+        // a caller's upper bound (the cost of a schedule it already has), with the same margin
+        if (ub_ext < INFINITY) { UBT = fmin(UBT, ub_ext + TOL_P * (1.0 + fabs(ub_ext) + qabs)); gok = true; }
+        if (!gok) prune = false;
     }
     if (nodom && !prune) return nodom && (pos && neg) ? -1 : -2;
+    const int capn = prune ? CAPB : CAP;             // front capacity (overflow: -3)
     // the front stores each label's exact STATE x (not its key dx * x) and cost
     double2* fa = B.fa;
     double2* fb = B.fb;
@@ -2441,9 +2481,9 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             const unsigned long long bal = __ballot(keep);
             const int slot = nn + __popcll(bal & below);
             nn += __popcll(bal);
-            if (keep && slot < (prune ? NF_BOUND : NF)) {
+            if (keep && slot < capn) {
                 fb[slot] = make_double2(xc, cc);
-                B.par[k * NB_CAP + slot] = (uint16_t)(i | (u << 12));
+                B.par[k * PS + slot] = (uint16_t)(i | (u << 12));
                 kmn = umin(kmn, vk); kmx = umax(kmx, vk);
                 cmn = umin(cmn, vc); cmx = umax(cmx, vc);
             }
@@ -2453,7 +2493,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
                                              (k == 0 ? (prune ? 1e8 : 0.0) * (sx == S_T ? 1.0 : 2.0) : 0.0);
 #endif
         if (nn == 0) return 0;                       // no child left inside the feasible set
-        if (nn > (prune ? NF_BOUND : NF)) return -3;  // front overflow
+        if (nn > capn) return -3;                    // front overflow
         // the next stage's state and cost ranges from the survivors' positions: the exact
         // position V of a value lies in [v - 1, v + 2], widened past the back-conversion's
         // rounding
@@ -2490,10 +2530,11 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         const int oi = __shfl_xor(bi, o);
         if (ob < best || (ob == best && oi >= 0 && (bi < 0 || oi < bi))) { best = ob; bi = oi; }
     }
+    if (best_out) *best_out = best;
     if (lane == 0) {
         int j = bi;
         for (int k = H - 1; k >= 0; --k) {
-            const int p = B.par[k * NB_CAP + j];
+            const int p = B.par[k * PS + j];
             B.x[k * 8 + sv] = (double)(p >> 12);
             j = p & 0xFFF;
         }
@@ -2674,33 +2715,32 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
     return true;
 }
 
-// The direct path is two launches over the same homes.  DM_FRONT (the hot one) runs the exact
-// front DP only; a home where it does not apply (mixed-sign prices, a too-narrow feasible
-// set, front overflow, S != 6) is flagged in the workspace and left untouched (nothing of
-// its hash written).  DM_BUCKET then solves exactly the flagged homes, each chain by the front
-// DP where it applies and by the bucketed DP otherwise.  Keeping the rarely needed bucketed DP
-// out of DM_FRONT keeps its register allocation out of the hot kernel.
+// The direct path is two launches.  DM_FRONT (the hot one, one block per home) runs the exact
+// front DP with fronts of up to NF labels (NF_BOUND with the LP bound).  A home where it does not
+// apply (front overflow -- stage-varying RL prices --, mixed-sign prices, a too-narrow feasible set,
+// S != 6) is appended to a list in the workspace and left untouched (nothing of its hash written).
+// DM_BUCKET, a persistent launch of SECOND_SLOTS blocks, then solves the listed homes: each chain
+// by the same front DP where it applies; otherwise by the bucketed DP (dp_thermal, an
+// approximation) whose schedule's cost then bounds an exact front DP with fronts of up to NF_BIG
+// labels (its own back-pointer rows per block), which replaces that schedule by the optimum.  Only
+// a chain that outgrows even NF_BIG keeps the bucketed schedule (int_path records it).  Keeping the
+// bucketed DP and the big pass out of DM_FRONT keeps their registers and LDS out of the hot kernel.
 enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1 };
 
 template <bool EXPLICIT, int MODE>
-__global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_kernel(KArgs a) {
+DEV void solve_direct(const KArgs& a, int home, double* smem, int slot) {
     constexpr int NT = WAVE;
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int home = blockIdx.x;
     const int lane = threadIdx.x;
     const int N = a.d.n_homes;
-    if (home >= N) return;
     const int H = a.d.horizon;
-    int* const defer = reinterpret_cast<int*>(reinterpret_cast<char*>(a.p.workspace) + par_region_bytes(N, H) +
-                                              (size_t)N * 8 * H * sizeof(double));
-    if (MODE == DM_BUCKET && defer[home] == 0) return;
+    char* const ws = reinterpret_cast<char*>(a.p.workspace);
+    int* const list = reinterpret_cast<int*>(ws + defer_offset(N, H));     // [N] + length at [N]
     Home h;
     LdsD D = carve_direct(smem, H, a.d.sub_steps);
-    D.par = reinterpret_cast<uint16_t*>(a.p.workspace) + (size_t)home * H * NB_CAP;
+    D.par = reinterpret_cast<uint16_t*>(ws) + (size_t)home * H * NB_CAP;
     // the stage-slot solution lives in the workspace too (after every home's back-pointers):
     // it is written once per chain and read by the cleanup, so LDS goes to the DP
-    D.x = reinterpret_cast<double*>(reinterpret_cast<char*>(a.p.workspace) + par_region_bytes(N, H)) +
-          (size_t)home * 8 * H;
+    D.x = reinterpret_cast<double*>(ws + par_region_bytes(N, H)) + (size_t)home * 8 * H;
     Lds L = lp_view(D);
     Io io{a.vals, a.fc, N, home};
     Prof pf;
@@ -2708,7 +2748,6 @@ __global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_ker
     if (prologue<EXPLICIT>(a, h, L, io, lane, NT, D.sc) == DRAGG_ST_ERR_MISSING) {
         if (lane == 0) {
             write_missing(a, home);
-            defer[home] = 0;
         }
         return;
     }
@@ -2744,6 +2783,12 @@ __global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_ker
         int changes = 0;
         for (int k = lane; k < H; k += NT) changes += (k > 0 && D.price[k] != D.price[k - 1]) ? 1 : 0;
         const bool use_bound = dpp_isum(changes) * 4 > H;
+        // such prices grow fronts past NF_BOUND at most homes (measured: 9,990 of 10,000 under
+        // an RL price): the hot launch hands these homes to the second one right away
+        if (MODE == DM_FRONT && use_bound) {
+            if (lane == 0) list[atomicAdd(list + N, 1)] = home;
+            return;
+        }
         for (int chain = 0; chain < 2 && ok; ++chain) {
             reload_home(h, a, home, saved);
             twlo0 = saved[6]; twhi0 = saved[7];
@@ -2771,23 +2816,60 @@ __global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_ker
             // the exact front DP; the bucketed DP only where it does not apply (mixed-sign
             // prices, a feasible set narrower than one duty step, front overflow, S != 6)
             int r = -1;
-            if (h.S == 6) {
-                double* const wl = reinterpret_cast<double*>(D.rmin + NF_BOUND);   // past the front
-                double2* const wg = reinterpret_cast<double2*>(reinterpret_cast<char*>(a.p.workspace) +
-                                                               w_region_offset(N, H)) + (size_t)home * (H + 1) * WAVE;
+            double2* const wg = reinterpret_cast<double2*>(ws + w_region_offset(N, H)) + (size_t)home * (H + 1) * WAVE;
+            if (h.S == 6 && !(MODE == DM_BUCKET && use_bound)) {
+                double* const wl = D.wl;
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
                                    wg, wl, wl + WAVE, wl + 2 * WAVE};
-                r = dp_front<6>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
+                r = dp_front<6, NF, NF_BOUND>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
+#ifdef DRAGG_FRONT_STATS2
+                // diagnostic: the T chain's fronts when the bound is the optimum itself
+                if (c0 && r == 1 && use_bound) {
+                    double best = INFINITY;
+                    dp_front<6, NF, NF_BOUND>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound, INFINITY, &best);
+                    for (int k = lane; k < H; k += NT) D.x[k * 8 + S_PAD] = 0.0;
+                    __syncthreads();
+                    r = dp_front<6, NF, NF_BOUND>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound, best);
+                }
+#endif
             }
             if (r >= 0) {
                 ok = r == 1;
             } else if (MODE == DM_FRONT) {                 // leave the home to DM_BUCKET
-                if (lane == 0) defer[home] = 1;
+                if (lane == 0) list[atomicAdd(list + N, 1)] = home;
                 return;
             } else {
-                int_path |= (1 << chain) | ((-r) << (4 + 4 * chain));   // chain bit + reason
                 ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
                               : dp_thermal<0>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
+                int r2 = r;
+                // the big pass, except for a feasible set narrower than one duty step (no
+                // dominance there: its fronts outgrow any capacity, measured)
+                if (h.S == 6 && r != -2) {
+                    // the exact pass with big fronts, bounded by the bucketed schedule's cost
+                    double ub = INFINITY;
+                    if (ok) {
+                        double c = 0.0;
+                        for (int k = lane; k < H; k += NT) c += D.cq[k] * D.x[k * 8 + sv];
+                        ub = dpp_sum(c);
+                    }
+                    const BigLayout bl = big_layout(H, a.d.sub_steps);
+                    char* const sb = reinterpret_cast<char*>(smem);
+                    double* const wl = reinterpret_cast<double*>(sb + bl.wl);
+                    uint16_t* const bpar = reinterpret_cast<uint16_t*>(ws + big_region_offset(N, H)) + (size_t)slot * H * NF_BIG;
+                    const FrontBufs FB{reinterpret_cast<double2*>(sb + bl.fa), reinterpret_cast<double2*>(sb + bl.fb),
+                                       reinterpret_cast<unsigned long long*>(sb + bl.kb),
+                                       reinterpret_cast<unsigned long long*>(sb + bl.cb),
+                                       reinterpret_cast<unsigned*>(sb + bl.mh), reinterpret_cast<unsigned*>(sb + bl.kl),
+                                       reinterpret_cast<unsigned*>(sb + bl.flo), reinterpret_cast<unsigned*>(sb + bl.fhi),
+                                       D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE};
+                    __syncthreads();
+                    // keeps the bucketed schedule in D.x unless it finds (and writes) the optimum
+                    r2 = dp_front<6, NF_BIG, NF_BIG, NF_BIG>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
+                    if (r2 == 1) ok = true;
+                    else if (r2 == 0 && !ok) ok = false;      // exact: no integer schedule
+                    else if (r2 == 0) r2 = -4;                // bound inconsistent with the schedule: keep it
+                }
+                if (r2 < 0) int_path |= (1 << chain) | ((-r2) << (4 + 4 * chain));   // chain bit + reason
             }
         }
         pf.mark(DRAGG_PH_INTEGER);
@@ -2816,8 +2898,7 @@ __global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_ker
         a.out.iters[home] = 0;
         a.out.obj[home] = obj;
         a.out.relax_obj[home] = NAN;
-        if (a.out.int_path) a.out.int_path[home] = int_path;
-        if (MODE == DM_FRONT) defer[home] = 0;
+        if (a.out.int_path) a.out.int_path[home] = int_path | (MODE == DM_BUCKET ? (1 << 12) : 0);
     }
     if (a.out.hist && lane == 0)      // lane 0 wrote every vals field of this home
         for (int k = 0; k < DRAGG_NVAL; ++k) a.out.hist[(size_t)k * N + home] = io.v(k);
@@ -2826,22 +2907,50 @@ __global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_ker
         for (int k = 0; k < DRAGG_NPHASE; ++k) a.out.cycles[(size_t)k * N + home] = (int64_t)pf.acc[k];
 }
 
-__global__ __launch_bounds__(256) void aggregate_kernel(const double* vals, int N, double* out3) {
-    __shared__ double red[3][256];
-    double s[3] = {0, 0, 0};
-    const int keys[3] = {DRAGG_K_P_GRID, DRAGG_K_FORECAST_P_GRID, DRAGG_K_COST};
-    for (int i = threadIdx.x; i < N; i += 256)
-        for (int c = 0; c < 3; ++c) {
-            s[c] += vals[(size_t)keys[c] * N + i];    // NaN (absent field) propagates
-        }
-    for (int c = 0; c < 3; ++c) red[c][threadIdx.x] = s[c];
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (threadIdx.x < w)
-            for (int c = 0; c < 3; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + w];
+template <bool EXPLICIT, int MODE>
+__global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_kernel(KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    if (MODE == DM_FRONT) {
+        if ((int)blockIdx.x < a.d.n_homes) solve_direct<EXPLICIT, MODE>(a, blockIdx.x, smem, 0);
+        return;
+    }
+    // persistent: block b solves the deferred homes b, b + gridDim.x, ... of the list (its own
+    // back-pointer rows: slot b); every block reaches the end of the list and exits
+    const int* const list = reinterpret_cast<const int*>(reinterpret_cast<const char*>(a.p.workspace) +
+                                                         defer_offset(a.d.n_homes, a.d.horizon));
+    const int cnt = min(list[a.d.n_homes], a.d.n_homes);
+    for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
+        const int home = list[j];
+        if (home < 0 || home >= a.d.n_homes) continue;
+        solve_direct<EXPLICIT, MODE>(a, home, smem, blockIdx.x);
         __syncthreads();
     }
-    if (threadIdx.x < 3) out3[threadIdx.x] = red[threadIdx.x][0];
+}
+
+// collect_data's three sums (aggregator.py:728-755) in one 1024-thread block: 16 waves of
+// independent loads (a step's sums are a latency-bound 240 KB read at 10k homes), then a wave
+// reduction and a pass over the 16 wave partials
+constexpr int AGG_NT = 1024;
+__global__ __launch_bounds__(AGG_NT) void aggregate_kernel(const double* vals, int N, double* out3) {
+    __shared__ double red[3][AGG_NT / WAVE];
+    const double* p0 = vals + (size_t)DRAGG_K_P_GRID * N;
+    const double* p1 = vals + (size_t)DRAGG_K_FORECAST_P_GRID * N;
+    const double* p2 = vals + (size_t)DRAGG_K_COST * N;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int i = threadIdx.x; i < N; i += AGG_NT) {   // NaN (absent field) propagates
+        s0 += p0[i];
+        s1 += p1[i];
+        s2 += p2[i];
+    }
+    s0 = dpp_sum(s0); s1 = dpp_sum(s1); s2 = dpp_sum(s2);
+    const int w = threadIdx.x / WAVE;
+    if ((threadIdx.x & (WAVE - 1)) == 0) { red[0][w] = s0; red[1][w] = s1; red[2][w] = s2; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        double t = 0.0;
+        for (int i = 0; i < AGG_NT / WAVE; ++i) t += red[threadIdx.x][i];
+        out3[threadIdx.x] = t;
+    }
 }
 
 __global__ void noise_kernel(int N, int H, uint64_t seed, int off, int stride, int t, double* out) {
@@ -2858,10 +2967,11 @@ __global__ void noise_kernel(int N, int H, uint64_t seed, int off, int stride, i
 bool direct_mode(const dragg_mpc_dims* d) { return d->int_mode == DRAGG_INT_ROUND; }
 
 size_t workspace_bytes(const dragg_mpc_dims* d) {
-    // direct: [N][H][NB_CAP] u16 back-pointers, [N][8H] f64 solutions, [N] i32 DM_BUCKET flags,
-    // [N][H+1][64] LP cost-to-go rows; round_lp: the back-pointers of its front DP
+    // direct: [N][H][NB_CAP] u16 back-pointers, [N][8H] f64 solutions, the [N + 1] i32 list of
+    // deferred homes, [N][H+1][64] LP cost-to-go rows, the second launch's [SECOND_SLOTS][H][NF_BIG]
+    // u16 back-pointers; round_lp: the back-pointers of its front DP
     if (d->int_mode == DRAGG_INT_ROUND_LP) return par_region_bytes(d->n_homes, d->horizon);
-    return direct_mode(d) ? w_region_offset(d->n_homes, d->horizon) + w_region_bytes(d->n_homes, d->horizon) : 0;
+    return direct_mode(d) ? big_region_offset(d->n_homes, d->horizon) + big_region_bytes(d->horizon) : 0;
 }
 
 size_t kernel_lds_bytes(const dragg_mpc_dims* d) {
@@ -2874,11 +2984,12 @@ int check_dims(const dragg_mpc_dims* d) {
     if (direct_mode(d) && d->sub_steps > 15) return DRAGG_E_ARG;     // 4-bit duty in the DP record
     if (direct_mode(d) && !direct_fits(d->horizon)) return DRAGG_E_HORIZON;
     if (kernel_lds_bytes(d) > 160 * 1024) return DRAGG_E_HORIZON;
+    if (direct_mode(d) && big_layout(d->horizon, d->sub_steps).bytes > 160 * 1024) return DRAGG_E_HORIZON;
     return DRAGG_OK;
 }
 
 template <typename K>
-int launch_kernel(K kern, int& attr_state, const KArgs& a, int nt, hipStream_t s) {
+int launch_kernel(K kern, int& attr_state, const KArgs& a, int blocks, int nt, size_t lds, hipStream_t s) {
     if (!attr_state) {
         if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
             hipSuccess)
@@ -2886,17 +2997,23 @@ int launch_kernel(K kern, int& attr_state, const KArgs& a, int nt, hipStream_t s
         attr_state = 1;
     }
     if (a.d.n_homes == 0) return DRAGG_OK;
-    hipLaunchKernelGGL(kern, dim3(a.d.n_homes), dim3(nt), kernel_lds_bytes(&a.d), s, a);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(nt), lds, s, a);
     return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
 }
 
 template <bool EXPLICIT>
 int launch(const KArgs& a, hipStream_t s) {
     static int attr[4] = {0, 0, 0, 0};
-    if (!direct_mode(&a.d)) return launch_kernel(mpc_home_kernel<EXPLICIT>, attr[0], a, 64, s);
-    const int rc = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT>, attr[1], a, WAVE, s);
+    const int N = a.d.n_homes;
+    if (!direct_mode(&a.d)) return launch_kernel(mpc_home_kernel<EXPLICIT>, attr[0], a, N, 64, kernel_lds_bytes(&a.d), s);
+    if (N == 0) return DRAGG_OK;
+    // the deferred list starts empty (its length word), then the hot launch, then the second
+    int* const len = reinterpret_cast<int*>(reinterpret_cast<char*>(a.p.workspace) + defer_offset(N, a.d.horizon)) + N;
+    if (hipMemsetAsync(len, 0, sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
+    const int rc = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT>, attr[1], a, N, WAVE, kernel_lds_bytes(&a.d), s);
     if (rc) return rc;
-    return launch_kernel(mpc_direct_kernel<EXPLICIT, DM_BUCKET>, attr[2], a, WAVE, s);
+    return launch_kernel(mpc_direct_kernel<EXPLICIT, DM_BUCKET>, attr[2], a, min(N, SECOND_SLOTS), WAVE,
+                         (size_t)big_layout(a.d.horizon, a.d.sub_steps).bytes, s);
 }
 
 }  // namespace
@@ -2967,7 +3084,7 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
 int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, double* out3, void* stream) {
     // n_homes == 0: the sums are zero (vals may be NULL)
     if (!dims || !hash || (!hash->vals && dims->n_homes > 0) || !out3 || dims->n_homes < 0) return DRAGG_E_ARG;
-    hipLaunchKernelGGL(aggregate_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, hash->vals,
+    hipLaunchKernelGGL(aggregate_kernel, dim3(1), dim3(AGG_NT), 0, (hipStream_t)stream, hash->vals,
                        dims->n_homes, out3);
     return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
 }

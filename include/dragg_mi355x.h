@@ -161,7 +161,9 @@ typedef struct dragg_mpc_out {
                                    = the indoor-air / tank chain used the bucketed
                                    approximation; bits 4-7 / 8-11 its reason: 1 mixed-sign
                                    prices, 2 a feasible set narrower than one duty step,
-                                   3 front overflow                                      */
+                                   3 front overflow; bit 12 = solved by the second launch
+                                   (its front outgrew the hot launch's capacity; still
+                                   exact when bits 0-11 are 0)                           */
 } dragg_mpc_out;
 
 /* solver phases timed into dragg_mpc_out.cycles (diagnostic; NULL = not stamped) */

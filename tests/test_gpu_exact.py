@@ -43,7 +43,7 @@ def _solve(d, mode="round"):
     b.vals.copy_(torch.tensor(vals))
     b.solve_explicit(**ex)
     torch.cuda.synchronize()
-    return dict(status=b.status.cpu().numpy(), fc=b.fc.cpu().numpy(), path=b.int_path.cpu().numpy(), S=b.S)
+    return dict(status=b.status.cpu().numpy(), fc=b.fc.cpu().numpy(), path=b.int_path.cpu().numpy() & L.PATH_APPROX_MASK, S=b.S)
 
 
 def _thermal_cost(r, fc, i, S):

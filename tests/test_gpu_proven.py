@@ -46,7 +46,7 @@ def _solved():
         b.solve_explicit(**ex)
         torch.cuda.synchronize()
         _RES["r"] = (d, dict(status=b.status.cpu().numpy(), obj=b.obj.cpu().numpy(), fc=b.fc.cpu().numpy(),
-                             path=b.int_path.cpu().numpy(), S=b.S, H=b.H))
+                             path=b.int_path.cpu().numpy() & L.PATH_APPROX_MASK, S=b.S, H=b.H))
     return _RES["r"]
 
 

@@ -152,11 +152,13 @@ def test_size_queries_without_gpu(lib_path):
                int_mode=L.INT_ROUND, max_iter=0, check_every=0, discount=0.92)
     ws = lib.dragg_mpc_workspace_bytes(ctypes.byref(d))
     # u16 back-pointer per front label and stage (NB_CAP = 336), rounded to 256 B, then the
-    # [N][8H] f64 stage-slot solutions and the [N] i32 flags of the bucketed second launch, then
-    # (256-aligned) the front DP's LP cost-to-go rows [N][H + 1][64] (x, v)
+    # [N][8H] f64 stage-slot solutions and the [N] i32 list (+ its length) of the homes deferred to
+    # the second launch, then (256-aligned) the front DP's LP cost-to-go rows [N][H + 1][64] (x, v),
+    # then (256-aligned) the second launch's back-pointer rows [512 blocks][H][NF_BIG = 2048] u16
     par = (100 * 24 * 336 * 2 + 255) // 256 * 256
-    w_off = (par + 100 * 8 * 24 * 8 + 100 * 4 + 255) // 256 * 256
-    assert ws == w_off + 100 * 25 * 64 * 16
+    w_off = (par + 100 * 8 * 24 * 8 + 101 * 4 + 255) // 256 * 256
+    big_off = (w_off + 100 * 25 * 64 * 16 + 255) // 256 * 256
+    assert ws == big_off + 512 * 24 * 2048 * 2
     lds_direct = lib.dragg_mpc_lds_bytes(ctypes.byref(d))
     assert 0 < lds_direct <= 20 * 1024                 # 8 homes per CU at H = 24
     d.horizon = 48
