@@ -139,6 +139,43 @@ class DeviceAggregator:
             torch.distributed.all_reduce(out, group=self.group)
         return out
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    # The reference has no resume (aggregator.py:265-267, 768: a stopped run starts over); here a
+    # checkpoint is the device state a step reads -- the hash arrays, the timestep, the reward
+    # price -- plus the histories, one file per rank.  The season-noise stream is keyed by
+    # (seed, home, t), so a resumed run continues bit for bit as if it had not stopped.
+    def save_state(self, path):
+        t = self.timestep
+        state = {"timestep": t, "rank": self.rank, "world": self.world, "n_local": int(self.batch.N),
+                 "vals": self.batch.vals.cpu(), "fc": self.batch.fc.cpu(),
+                 "reward_price": self.batch.rp.cpu(),
+                 "agg_hist": self.agg_hist[:t].cpu(), "status_hist": self.status_hist[:t].cpu(),
+                 "deferred": torch.as_tensor(self._deferred, dtype=torch.long),
+                 "hist": self.hist[:t].cpu() if self.hist is not None else None}
+        tmp = path + ".tmp"
+        torch.save(state, tmp)
+        import os
+        os.replace(tmp, path)                 # a crash mid-write leaves the previous checkpoint
+        return path
+
+    def load_state(self, path):
+        """Resume from save_state's file (tensors only: loaded with weights_only=True)."""
+        st = torch.load(path, map_location="cpu", weights_only=True)
+        if (st["rank"], st["world"], st["n_local"]) != (self.rank, self.world, int(self.batch.N)):
+            raise ValueError(f"checkpoint {path} is for rank {st['rank']} of {st['world']} with "
+                             f"{st['n_local']} homes, not rank {self.rank} of {self.world} with {self.batch.N}")
+        t = int(st["timestep"])
+        self.batch.vals.copy_(st["vals"])
+        self.batch.fc.copy_(st["fc"])
+        self.batch.set_reward_price(st["reward_price"].to(self.device))
+        self.agg_hist[:t].copy_(st["agg_hist"])
+        self.status_hist[:t].copy_(st["status_hist"])
+        self._deferred = st["deferred"].tolist()
+        if self.hist is not None and st["hist"] is not None:
+            self.hist[:t].copy_(st["hist"])
+        self.timestep = t
+        return t
+
     def check_errors(self):
         """Raise as the reference would if a home hit a crashing path (KeyError / ValueError)."""
         st = self.status_hist[:self.timestep].cpu().numpy()

@@ -96,6 +96,7 @@ class Aggregator:
         """The checked homes (aggregator.py:762-765 / 879-882) as this rank's device shard."""
         from .aggregator import DeviceAggregator
         self.checked = [h for h in self.all_homes if self.check_type == "all" or h["type"] == self.check_type]
+        self._hist_rows = 0                 # steps of the history already on rank 0 (_history)
         col = lambda c: self.all_data[c].to_numpy(dtype=float)  # noqa: E731
         self.dev = DeviceAggregator(self.checked, col("OAT"), col("GHI"), col("tou"), self.start_hour_index,
                                     self.num_timesteps, reward_price=self.reward_price, int_mode=self.int_mode,
@@ -104,13 +105,25 @@ class Aggregator:
                                     **({"batch_cls": self.batch_cls} if self.batch_cls else {}))
         return self.dev
 
+    def state_path(self):
+        """This rank's device-state checkpoint, next to results.json (<run dir>/<case>/)."""
+        d = os.path.join(self.run_dir, self.case)
+        os.makedirs(d, exist_ok=True)
+        return os.path.join(d, f"state-rank{self.rank}-of-{self.world}.pt")
+
     # aggregator.py:757-778
-    def run_baseline(self, noise_fn=None):
+    def run_baseline(self, noise_fn=None, resume=False):
         """`noise_fn(t)`, optional: the season draw [H][homes checked] of step t (replaces the
-        keyed on-device stream, e.g. to replay a recorded run)."""
+        keyed on-device stream, e.g. to replay a recorded run).  Every checkpoint also saves
+        each rank's device state; `resume=True` continues from it (the reference has no resume:
+        aggregator.py:265-267, 768) and finishes with the results an uninterrupted run writes."""
         self.start_time = datetime.now()
         self._device_community()
-        for t in range(self.num_timesteps):
+        t0 = 0
+        if resume and os.path.isfile(self.state_path()):
+            t0 = self.dev.load_state(self.state_path())
+            self.timestep = t0
+        for t in range(t0, self.num_timesteps):
             noise = noise_fn(t)[:, self.dev.index] if noise_fn is not None else None
             self.dev.run_iteration(noise)
             self.dev.collect_data(defer=True)      # no feedback: the sums are reduced at the end
@@ -121,6 +134,9 @@ class Aggregator:
                 # out of every results.json written
                 self.dev.check_errors()
                 self.write_outputs()
+                self.dev.save_state(self.state_path())
+                if getattr(self, "stop_after", None) is not None and t + 1 >= self.stop_after:
+                    return                         # (tests: a run interrupted after a checkpoint)
         self.dev.reduce_history()
         self.dev.check_errors()
 
@@ -242,19 +258,44 @@ class Aggregator:
         return self.write_outputs()
 
     def _history(self):
-        """The checked homes' hash history [T][19][N] on rank 0 (gathered from every rank)."""
-        hist = self.dev.hist[:self.dev.timestep].cpu().numpy()
-        if self.world == 1:
-            return hist
-        import torch.distributed as dist
-        parts = [None] * self.world if self.rank == 0 else None
-        dist.gather_object(hist, parts, dst=0, group=self.group)
+        """The checked homes' hash history [T][19][N] on rank 0.
+
+        Incremental: each call brings over only the steps since the previous one (a checkpoint
+        then costs its own rows, not the whole run again), as one tensor gather of the shards
+        padded to a common width (NCCL on the device, gloo on the host) -- no pickling."""
+        T = self.dev.timestep
+        t0 = getattr(self, "_hist_rows", 0)
+        if t0 == 0:
+            self._hist_host = []
+        if T > t0:
+            new = self.dev.hist[t0:T]                      # [dT][19][n_local]
+            if self.world == 1:
+                self._hist_host.append(new.cpu().numpy())
+            else:
+                import torch
+                import torch.distributed as dist
+                n_all = len(self.checked)
+                width = -(-n_all // self.world)            # the widest strided shard
+                on_dev = dist.get_backend(self.group) == "nccl"
+                src = new if on_dev else new.cpu()
+                pad = torch.full(src.shape[:2] + (width,), float("nan"), dtype=src.dtype, device=src.device)
+                pad[:, :, :src.shape[2]] = src
+                parts = [torch.empty_like(pad) for _ in range(self.world)] if self.rank == 0 else None
+                dist.gather(pad, parts, dst=0, group=self.group)
+                if self.rank == 0:
+                    out = np.empty(src.shape[:2] + (n_all,), dtype=np.float64)
+                    for r, p in enumerate(parts):          # rank r holds homes r, r + world, ... (shard_index)
+                        k = len(range(r, n_all, self.world))
+                        out[:, :, r::self.world] = p[:, :, :k].cpu().numpy()
+                    self._hist_host.append(out)
+            self._hist_rows = T
         if self.rank != 0:
             return None
-        out = np.empty(hist.shape[:2] + (len(self.checked),), dtype=hist.dtype)
-        for r, p in enumerate(parts):          # rank r holds homes r, r + world, ... (shard_index)
-            out[:, :, r::self.world] = p
-        return out
+        if not self._hist_host:
+            return np.empty((0, self.dev.hist.shape[1], len(self.checked)))
+        if len(self._hist_host) > 1:
+            self._hist_host = [np.concatenate(self._hist_host, axis=0)]
+        return self._hist_host[0]
 
     # aggregator.py:783-844 (summarize_baseline + write_outputs)
     def write_outputs(self):
@@ -278,7 +319,7 @@ class Aggregator:
         return R.write_results(self.run_dir, self.case, collected)
 
     # aggregator.py:941-970
-    def run(self, noise_fn=None):
+    def run(self, noise_fn=None, resume=False):
         sim = self.config["simulation"]
         self.checkpoint_interval = R.checkpoint_interval(sim["checkpoint_interval"], self.dt)
         self.version = sim["named_version"]
@@ -290,7 +331,7 @@ class Aggregator:
             self.case = "baseline"
             self.flush()
             self.get_homes()
-            self.run_baseline(noise_fn)
+            self.run_baseline(noise_fn, resume=resume)
             return self.write_outputs()
         if sim.get("run_rl_agg"):
             from .rl import agent_policy

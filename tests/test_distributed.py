@@ -119,15 +119,17 @@ def _runner_worker(rank, world, port, root, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from dragg_amd.runner import Aggregator
     a = Aggregator(data_dir=os.path.join(root, "data"), outputs_dir=os.path.join(root, "outputs"),
-                   device=torch.device("cpu"), batch_cls=HashBatch)
+                   device=torch.device("cpu"), batch_cls=StateBatch)
     path = a.run()
     q.put((rank, a.dev.index.tolist(), path))
     dist.destroy_process_group()
 
 
-def test_runner_two_ranks_gathers_history(tmp_path):
+@pytest.mark.parametrize("checkpoint", ["daily", "hourly"])
+def test_runner_two_ranks_gathers_history(tmp_path, checkpoint):
     """Two ranks each solve a strided shard; rank 0 gathers the hash history and writes
-    results.json with every home's series in community order."""
+    results.json with every home's series in community order.  Hourly checkpoints (every 4
+    steps) gather the history in three increments."""
     import json
     from tests import fixtures as F
     from tests.test_runner import _synthetic_data
@@ -137,7 +139,7 @@ def test_runner_two_ranks_gathers_history(tmp_path):
     params = dict(n=7, batt=2, pv=2, pvb=1, start="2015-01-01 00", end="2015-01-01 03", dt=4, horizon=2,
                   action_horizon=2, seed=3)
     with open(data / "config.toml", "w") as f:
-        f.write(F.config_text(params))
+        f.write(F.config_text(params).replace('checkpoint_interval = "daily"', f'checkpoint_interval = "{checkpoint}"'))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -156,3 +158,45 @@ def test_runner_two_ranks_gathers_history(tmp_path):
     for i, n in enumerate(names):
         assert out[n]["p_grid_opt"] == [i + 100.0 * t for t in range(T)]
     assert out["Summary"]["p_grid_aggregate"] == [sum(i + 100.0 * t for i in range(7)) for t in range(T)]
+
+
+class StateBatch(HashBatch):
+    """HashBatch with the solver state a checkpoint holds (hash arrays, reward price)."""
+
+    def __init__(self, homes, *a, **kw):
+        super().__init__(homes, *a, **kw)
+        self.vals = torch.zeros((19, self.N), dtype=torch.float64)
+        self.fc = torch.zeros((15, 4, self.N), dtype=torch.float64)
+        self.rp = torch.zeros(1, dtype=torch.float64)
+
+    def step(self, t, noise=None, hist=None):
+        super().step(t, noise, hist)
+        self.vals += t + self.gidx                 # state that depends on every previous step
+        self.fc[0] = self.vals[0]
+
+    def set_reward_price(self, rp):
+        self.rp = rp.clone()
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    """save_state / load_state (CPU): a run resumed from a mid-run checkpoint ends in the state
+    and histories of the uninterrupted run."""
+    from dragg_amd.aggregator import DeviceAggregator
+    homes = [{"name": f"h{i}"} for i in range(5)]
+    kw = dict(num_timesteps=6, device=torch.device("cpu"), batch_cls=StateBatch)
+    full = DeviceAggregator(homes, [0.0], [0.0], [0.0], **kw)
+    full.set_reward_price([0.25])
+    full.run_baseline()
+    part = DeviceAggregator(homes, [0.0], [0.0], [0.0], **kw)
+    part.set_reward_price([0.25])
+    part.run_baseline(steps=3)
+    path = part.save_state(str(tmp_path / "state.pt"))
+    res = DeviceAggregator(homes, [0.0], [0.0], [0.0], **kw)
+    assert res.load_state(path) == 3
+    assert float(res.batch.rp[0]) == 0.25
+    res.run_baseline()
+    assert torch.equal(res.batch.vals, full.batch.vals) and torch.equal(res.batch.fc, full.batch.fc)
+    assert torch.equal(res.hist, full.hist) and torch.equal(res.agg_hist, full.agg_hist)
+    other = DeviceAggregator(homes, [0.0], [0.0], [0.0], rank=1, world=2, **kw)
+    with pytest.raises(ValueError):
+        other.load_state(path)

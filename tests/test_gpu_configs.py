@@ -235,7 +235,12 @@ def test_config4_rl_10k_homes_price_broadcast_and_rollouts(gpu):
     agg.set_reward_price([x + 0.2 for x in rp])
     assert not torch.equal(agg.forecast(1), fc[:1])
     fb = np.array(fb)
-    print(f"configs[4]: {n_off} of {int((st == 0).sum())} optimal homes left the exact front DP (front overflow "
-          f"under the smooth RL price); sampled fallback gaps to the exact optimum: {len(fb)}, mean "
+    n_second = int((path[st == 0] & L.PATH_SECOND != 0).sum())
+    print(f"configs[4]: {n_second} of {int((st == 0).sum())} optimal homes solved by the second launch (big "
+          f"exact fronts under the smooth RL price), {n_off} of them left the exact DP (front overflow past "
+          f"NF_BIG); sampled fallback gaps to the exact optimum: {len(fb)}, mean "
           f"{fb.mean() if len(fb) else 0:.1e}, max {fb.max() if len(fb) else 0:.1e}")
+    # exactness under RL prices: at most 0.1 % of the homes may outgrow the big fronts (measured:
+    # 0 of 10,000 here, 3 of 80,000 over 8 RL steps, tools/count_paths.py)
+    assert n_off <= 0.001 * int((st == 0).sum()), n_off
     _report("configs[4] RL 10k homes, H = 48, July, rollout = commit", agg, homes, [(t,) + res], min_opt=0)

@@ -114,3 +114,38 @@ def test_runner_end_to_end(gpu, tmp_path):
     direct = dev.collected_data()
     for n in names:
         assert direct[n] == res[n], n
+
+
+@pytest.mark.gpu
+def test_runner_resume_from_checkpoint(gpu, tmp_path):
+    """A run stopped after a checkpoint and resumed from the saved device state writes the
+    results.json of an uninterrupted run, value for value (the noise stream is keyed by step)."""
+    from dragg_amd.runner import Aggregator
+    data = tmp_path / "data"
+    data.mkdir()
+    _synthetic_data(str(data))
+    params = dict(n=12, batt=3, pv=3, pvb=2, start="2015-01-01 00", end="2015-01-01 06", dt=4, horizon=6,
+                  action_horizon=6, seed=23)
+    _write_config(data / "config.toml", params)
+    with open(data / "config.toml") as f:
+        txt = f.read().replace('checkpoint_interval = "daily"', 'checkpoint_interval = "hourly"')
+    with open(data / "config.toml", "w") as f:
+        f.write(txt)
+    full = Aggregator(data_dir=str(data), outputs_dir=str(tmp_path / "full")).run()
+    a = Aggregator(data_dir=str(data), outputs_dir=str(tmp_path / "split"))
+    a.stop_after = 8                                  # "crash" after the second hourly checkpoint
+    a.run()
+    assert os.path.isfile(a.state_path())
+    b = Aggregator(data_dir=str(data), outputs_dir=str(tmp_path / "split"))
+    path = b.run(resume=True)
+    with open(full) as f:
+        want = json.load(f)
+    with open(path) as f:
+        got = json.load(f)
+    for k in want:
+        if k == "Summary":
+            for s in want[k]:
+                if s != "solve_time":
+                    assert got[k][s] == want[k][s], s
+        else:
+            assert got[k] == want[k], k
