@@ -36,7 +36,7 @@ constexpr int NF_BOUND = 240;           // ... when the LP bound is on: its W ta
 static_assert((NB_CAP + 8 - NF_BOUND) * 16 >= 3 * 64 * 8, "the W table lives in rmin past the front");
 constexpr int NF_BIG = 2048;            // front capacity of the second launch's exact pass
 constexpr int SECOND_SLOTS = 512;       // blocks of the persistent second launch (2 per CU)
-constexpr int NTB = 256;             // key buckets and cost buckets per stage (dp_front)
+constexpr int NTB = 192;             // key buckets and cost buckets per stage (dp_front)
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
 
 constexpr double SIGMA = 1e-6;
@@ -2779,13 +2779,16 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot) {
         // chain 1: water heater given T (mpc_calc.py:330-332).  One DP instantiation for both.
         bool ok = true;
         // prices that change at more than a quarter of the stages (RL reward prices; a tariff
-        // changes a few times a day): the front DP runs with its LP bound
+        // changes a few times a day) grow fronts past NF_BOUND at most homes (measured: 9,990 of
+        // 10,000): the hot launch hands these homes to the second one right away, which prunes
+        // with the LP bound.  (Pruning by bound at every tariff boundary too: -14 % latency of
+        // the slowest homes over the first 48 steps of the bench, but +13 % time over all 96.)
         int changes = 0;
         for (int k = lane; k < H; k += NT) changes += (k > 0 && D.price[k] != D.price[k - 1]) ? 1 : 0;
-        const bool use_bound = dpp_isum(changes) * 4 > H;
-        // such prices grow fronts past NF_BOUND at most homes (measured: 9,990 of 10,000 under
-        // an RL price): the hot launch hands these homes to the second one right away
-        if (MODE == DM_FRONT && use_bound) {
+        changes = dpp_isum(changes);
+        const bool rl_prices = changes * 4 > H;
+        const bool use_bound = rl_prices;
+        if (MODE == DM_FRONT && rl_prices) {
             if (lane == 0) list[atomicAdd(list + N, 1)] = home;
             return;
         }
@@ -2817,7 +2820,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot) {
             // prices, a feasible set narrower than one duty step, front overflow, S != 6)
             int r = -1;
             double2* const wg = reinterpret_cast<double2*>(ws + w_region_offset(N, H)) + (size_t)home * (H + 1) * WAVE;
-            if (h.S == 6 && !(MODE == DM_BUCKET && use_bound)) {
+            if (h.S == 6 && !(MODE == DM_BUCKET && rl_prices)) {
                 double* const wl = D.wl;
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
                                    wg, wl, wl + WAVE, wl + 2 * WAVE};

@@ -1,5 +1,3 @@
 set -o pipefail
-mkdir -p gpurun_out/s4
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rP --timeout 300 --timeout-method thread > gpurun_out/s4/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -60 gpurun_out/s4/pytest.log; exit 1; }
-tail -1 gpurun_out/s4/pytest.log
-grep "configs\[4\]" gpurun_out/s4/pytest.log
+BENCH_ARGS="--steps 96" bash tools/gpu_bench_ab.sh head c11 c11n128 c11n256 || exit 1
+BENCH_ARGS="--steps 96 --homes 1250" bash tools/gpu_bench_ab.sh head c11 c8 || exit 1
