@@ -36,6 +36,7 @@ constexpr int NF_BOUND = 240;           // ... when the LP bound is on: its W ta
 static_assert((NB_CAP + 8 - NF_BOUND) * 16 >= 3 * 64 * 8, "the W table lives in rmin past the front");
 constexpr int NF_BIG = 2048;            // front capacity of the second launch's exact pass
 constexpr int SECOND_SLOTS = 512;       // blocks of the persistent second launch (2 per CU)
+constexpr int PRUNE_AT = 96;            // front size that switches on the LP-bound pruning
 constexpr int NTB = 192;             // key buckets and cost buckets per stage (dp_front)
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
 
@@ -2259,8 +2260,10 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     //     More than 64 points, or a degenerate stage: no bound (exact all the same).
     //     On by request (prices that change at most stages: fronts grow large without it) and
     //     wherever dominance is off; the plain front DP is cheaper on piecewise-constant tariffs.
-    bool prune = B.wg != nullptr && (use_bound || nodom);
-    if (prune) {
+    double UBT = INFINITY;
+    auto make_bound = [&]() -> bool {
+    bool prune = true;
+    {
         double bl = H == 1 ? lo0 : lo, bh = H == 1 ? hi0 : hi;
         bl -= tw(bl);
         bh += tw(bh);
@@ -2314,7 +2317,6 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     // (d) an upper bound: the cost of one feasible schedule, greedy in q u + W_{k+1}(x') (the
     //     labels' own arithmetic).  Children with cost + W > bound (+ a margin past rounding)
     //     cannot lead to the optimum and are dropped.
-    double UBT = INFINITY;
     if (prune) {
         double qabs = 0.0;
         for (int k = lane; k < H; k += WAVE) qabs += fabs(B.cq[k]) * SS;
@@ -2350,8 +2352,12 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         if (ub_ext < INFINITY) { UBT = fmin(UBT, ub_ext + TOL_P * (1.0 + fabs(ub_ext) + qabs)); gok = true; }
         if (!gok) prune = false;
     }
+    return prune;
+    };
+    bool prune = B.wg != nullptr && (use_bound || nodom) && make_bound();
     if (nodom && !prune) return nodom && (pos && neg) ? -1 : -2;
-    const int capn = prune ? CAPB : CAP;             // front capacity (overflow: -3)
+    int capn = prune ? CAPB : CAP;                   // front capacity (overflow: -3)
+    bool tried = prune || B.wg == nullptr;           // the bound is built at most once
     // the front stores each label's exact STATE x (not its key dx * x) and cost
     double2* fa = B.fa;
     double2* fb = B.fb;
@@ -2368,6 +2374,19 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     }
     __syncthreads();
     for (int k = 0; k < H; ++k) {
+        // a front past PRUNE_AT labels (a tariff boundary inside the horizon): build the LP
+        // bound now and prune the remaining stages by it.  Only while the front fits the bounded
+        // capacity (the W table's LDS follows it) -- and, when fa is that buffer, stays clear of it.
+        if (!tried && n > PRUNE_AT && n <= CAPB) {
+            tried = true;
+            if (make_bound()) {
+                prune = true;
+                capn = CAPB;
+                w_to_lds(B, lane, B.wg[(k + 1) * WAVE + lane].x, B.wg[(k + 1) * WAVE + lane].y);
+                wnext = k + 2 <= H ? B.wg[(k + 2) * WAVE + lane] : make_double2(INFINITY, INFINITY);
+            }
+            __syncthreads();
+        }
         const double A = B.cA[k], C = B.cC[k], q = B.cq[k];
         double bl = k == 0 ? lo0 : lo, bh = k == 0 ? hi0 : hi;
         bl -= tw(bl);
