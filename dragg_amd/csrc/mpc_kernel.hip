@@ -2261,7 +2261,18 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     //     On by request (prices that change at most stages: fronts grow large without it) and
     //     wherever dominance is off; the plain front DP is cheaper on piecewise-constant tariffs.
     double UBT = INFINITY;
+    // W rows are stored and loaded only up to their point counts (lane j of wc0 / wc1 holds row j's
+    // / row 64 + j's count): no +inf padding goes through memory
+    int wc0 = 0, wc1 = 0;
+    auto set_count = [&](int j, int m) {
+        if ((j & (WAVE - 1)) == lane) { if (j < WAVE) wc0 = m; else wc1 = m; }
+    };
+    auto load_row = [&](int j) -> double2 {
+        const int m = j < WAVE ? read_lane(wc0, j) : read_lane(wc1, j - WAVE);
+        return lane < m ? B.wg[j * WAVE + lane] : make_double2(INFINITY, INFINITY);
+    };
     auto make_bound = [&]() -> bool {
+    if (H >= 2 * WAVE) return false;                 // row counts held for 128 rows (a 32 h horizon)
     bool prune = true;
     {
         double bl = H == 1 ? lo0 : lo, bh = H == 1 ? hi0 : hi;
@@ -2269,7 +2280,8 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         bh += tw(bh);
         double wx = lane == 0 ? bl : lane == 1 ? bh : INFINITY, wv = lane < 2 ? 0.0 : INFINITY;
         int m = 2;
-        B.wg[H * WAVE + lane] = make_double2(wx, wv);
+        if (lane < m) B.wg[H * WAVE + lane] = make_double2(wx, wv);
+        set_count(H, m);
         for (int j = H - 1; j >= 1; --j) {
             const double A = B.cA[j], C = B.cC[j], q = B.cq[j];
             if (!(A > 0.0) || m + 1 > WAVE) { prune = false; break; }
@@ -2311,7 +2323,8 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             wv = lane < m2 ? B.wlv[lane] : INFINITY;
             m = m2;
             __syncthreads();
-            B.wg[j * WAVE + lane] = make_double2(wx, wv);
+            if (lane < m) B.wg[j * WAVE + lane] = make_double2(wx, wv);
+            set_count(j, m);
         }
     }
     // (d) an upper bound: the cost of one feasible schedule, greedy in q u + W_{k+1}(x') (the
@@ -2323,9 +2336,9 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         qabs = dpp_sum(qabs);
         double gx = x0, ub = 0.0;
         bool gok = true;
-        double2 cur = B.wg[WAVE + lane];
+        double2 cur = load_row(1);
         for (int k = 0; k < H && gok; ++k) {
-            double2 nxt = k + 2 <= H ? B.wg[(k + 2) * WAVE + lane] : make_double2(INFINITY, INFINITY);
+            double2 nxt = k + 2 <= H ? load_row(k + 2) : make_double2(INFINITY, INFINITY);
             w_to_lds(B, lane, cur.x, cur.y);
             __syncthreads();
             const double A = B.cA[k], C = B.cC[k], q = B.cq[k];
@@ -2369,8 +2382,9 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     // W_{k+1} of the stage in the LDS table, W_{k+2} in flight
     double2 wnext = make_double2(INFINITY, INFINITY);
     if (prune) {
-        w_to_lds(B, lane, B.wg[WAVE + lane].x, B.wg[WAVE + lane].y);
-        if (H >= 2) wnext = B.wg[2 * WAVE + lane];
+        const double2 w1 = load_row(1);
+        w_to_lds(B, lane, w1.x, w1.y);
+        if (H >= 2) wnext = load_row(2);
     }
     __syncthreads();
     for (int k = 0; k < H; ++k) {
@@ -2382,8 +2396,9 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             if (make_bound()) {
                 prune = true;
                 capn = CAPB;
-                w_to_lds(B, lane, B.wg[(k + 1) * WAVE + lane].x, B.wg[(k + 1) * WAVE + lane].y);
-                wnext = k + 2 <= H ? B.wg[(k + 2) * WAVE + lane] : make_double2(INFINITY, INFINITY);
+                const double2 wk = load_row(k + 1);
+                w_to_lds(B, lane, wk.x, wk.y);
+                wnext = k + 2 <= H ? load_row(k + 2) : make_double2(INFINITY, INFINITY);
             }
             __syncthreads();
         }
@@ -2533,7 +2548,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         for (int b = lane; b < NTB && !nodom; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
         if (prune && k + 1 < H) {
             w_to_lds(B, lane, wnext.x, wnext.y);
-            if (k + 3 <= H) wnext = B.wg[(k + 3) * WAVE + lane];
+            if (k + 3 <= H) wnext = load_row(k + 3);
         }
         __syncthreads();
         double2* tmp = fa; fa = fb; fb = tmp;
