@@ -36,7 +36,9 @@ constexpr int NF_BOUND = 240;           // ... when the LP bound is on: its W ta
 static_assert((NB_CAP + 8 - NF_BOUND) * 16 >= 3 * 64 * 8, "the W table lives in rmin past the front");
 constexpr int NF_BIG = 2048;            // front capacity of the second launch's exact pass
 constexpr int SECOND_SLOTS = 512;       // blocks of the persistent second launch (2 per CU)
-constexpr int PRUNE_AT = 96;            // front size that switches on the LP-bound pruning
+constexpr int PRUNE_AT = 64;            // front size that switches on the LP-bound pruning
+constexpr int NF_HOT = 168;             // front capacity of the hot launch (front_layout): less LDS
+                                        //   per home, more homes per CU; a larger front defers
 constexpr int NTB = 192;             // key buckets and cost buckets per stage (dp_front)
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
 
@@ -1436,8 +1438,48 @@ struct DirectLayout {
     int draw, oat, ghi, price, cA, cC, cq, sc, t2, bx0, bp1, bp2, lab, rmin, tail;
     int kb, cb, mh, kl, flo, fhi;             // dp_front tail
     int cand, rt, candp, tarr, rsrc;          // dp_zspace tail
+    int wl, sgS, sgL;                         // front_layout only: W table, battery segment lists
     int bytes;
 };
+
+// The hot launch (DM_FRONT) runs only the front DP: fronts of NF_HOT labels, the W table, the
+// bucket arrays and hulls; the battery LP (after both chains) reuses that region.  Occupancy is
+// what this buys (8 -> 11 homes per CU at H = 48: 2.44 -> 2.13 ms per bench step; measured the
+// other way: 7 homes per CU cost +11 % time, 6 +43 %).
+__host__ __device__ inline DirectLayout front_layout(int H) {
+    DirectLayout o{};
+    int p = 0;
+    auto take = [&](int bytes, int align) { p = (p + align - 1) / align * align; const int r = p; p += bytes; return r; };
+    o.draw = take(8 * (H + 1), 16);
+    o.oat = take(8 * (H + 1), 8);
+    o.ghi = take(8 * (H + 1), 8);
+    o.price = take(8 * (H + 1), 8);
+    o.cA = take(8 * H, 8);
+    o.cC = take(8 * H, 8);
+    o.cq = take(8 * H, 8);
+    o.sc = take(8 * 32, 8);
+    o.tail = p;
+    o.lab = take(16 * NF_HOT, 16);
+    o.rmin = take(16 * NF_HOT, 16);
+    o.wl = take(8 * 3 * WAVE, 16);
+    o.kb = take(8 * NTB, 16);
+    o.cb = take(8 * NTB, 16);
+    o.mh = take(4 * NTB, 4);
+    o.kl = take(4 * NTB, 4);
+    o.flo = take(4 * (H + 1), 4);
+    o.fhi = take(4 * (H + 1), 4);
+    const int dp_end = p;
+    p = o.tail;                                  // the battery LP's arrays over the dead DP region
+    o.sgS = take(16 * seg_cap(H), 16);
+    o.sgL = take(16 * seg_cap(H), 16);
+    o.bx0 = take(8 * H, 8);
+    o.bp1 = take(8 * H, 8);
+    o.bp2 = take(8 * H, 8);
+    o.t2 = take(8 * H, 8);
+    o.cand = o.rt = o.candp = o.tarr = o.rsrc = -1;
+    o.bytes = (max(dp_end, p) + 15) / 16 * 16;
+    return o;
+}
 
 __host__ __device__ inline DirectLayout direct_layout(int H, int S) {
     DirectLayout o{};
@@ -1504,6 +1546,30 @@ __host__ __device__ inline BigLayout big_layout(int H, int S) {
     o.fhi = take(4 * (H + 1), 4);
     o.bytes = (max(p, d.bytes) + 15) / 16 * 16;
     return o;
+}
+
+DEV LdsD carve_front(double* smem, int H) {
+    const DirectLayout o = front_layout(H);
+    char* b = reinterpret_cast<char*>(smem);
+    auto D = [&](int off) { return reinterpret_cast<double*>(b + off); };
+    LdsD L{};
+    L.draw = D(o.draw); L.oat = D(o.oat); L.ghi = D(o.ghi); L.price = D(o.price);
+    L.x = nullptr;                                               // global workspace (kernel)
+    L.cA = D(o.cA); L.cC = D(o.cC); L.cq = D(o.cq);
+    L.sc = D(o.sc);
+    L.lab = reinterpret_cast<double2*>(b + o.lab);
+    L.rmin = reinterpret_cast<double2*>(b + o.rmin);
+    L.wl = D(o.wl);
+    L.kb = reinterpret_cast<unsigned long long*>(b + o.kb);
+    L.cb = reinterpret_cast<unsigned long long*>(b + o.cb);
+    L.mh = reinterpret_cast<unsigned*>(b + o.mh);
+    L.kl = reinterpret_cast<unsigned*>(b + o.kl);
+    L.flo = reinterpret_cast<unsigned*>(b + o.flo);
+    L.fhi = reinterpret_cast<unsigned*>(b + o.fhi);
+    L.sgS = D(o.sgS); L.sgL = D(o.sgL);
+    L.bx0 = D(o.bx0); L.bp1 = D(o.bp1); L.bp2 = D(o.bp2); L.t2 = D(o.t2);
+    L.par = nullptr;                                             // set by the kernel
+    return L;
 }
 
 DEV LdsD carve_direct(double* smem, int H, int S) {
@@ -2770,7 +2836,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot) {
     char* const ws = reinterpret_cast<char*>(a.p.workspace);
     int* const list = reinterpret_cast<int*>(ws + defer_offset(N, H));     // [N] + length at [N]
     Home h;
-    LdsD D = carve_direct(smem, H, a.d.sub_steps);
+    LdsD D = MODE == DM_FRONT ? carve_front(smem, H) : carve_direct(smem, H, a.d.sub_steps);
     D.par = reinterpret_cast<uint16_t*>(ws) + (size_t)home * H * NB_CAP;
     // the stage-slot solution lives in the workspace too (after every home's back-pointers):
     // it is written once per chain and read by the cleanup, so LDS goes to the DP
@@ -2858,7 +2924,8 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot) {
                 double* const wl = D.wl;
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
                                    wg, wl, wl + WAVE, wl + 2 * WAVE};
-                r = dp_front<6, NF, NF_BOUND>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
+                r = MODE == DM_FRONT ? dp_front<6, NF_HOT, NF_HOT>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound)
+                                     : dp_front<6, NF, NF_BOUND>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
 #ifdef DRAGG_FRONT_STATS2
                 // diagnostic: the T chain's fronts when the bound is the optimum itself
                 if (c0 && r == 1 && use_bound) {
@@ -3011,8 +3078,9 @@ size_t workspace_bytes(const dragg_mpc_dims* d) {
     return direct_mode(d) ? big_region_offset(d->n_homes, d->horizon) + big_region_bytes(d->horizon) : 0;
 }
 
+// per home, the hot launch's (int_mode round: DM_FRONT)
 size_t kernel_lds_bytes(const dragg_mpc_dims* d) {
-    return direct_mode(d) ? (size_t)direct_lds_bytes(d->horizon, d->sub_steps) : (size_t)lds_doubles(d->horizon) * 8;
+    return direct_mode(d) ? (size_t)front_layout(d->horizon).bytes : (size_t)lds_doubles(d->horizon) * 8;
 }
 
 int check_dims(const dragg_mpc_dims* d) {
