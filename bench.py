@@ -192,8 +192,9 @@ def extra_rooflines(pmc, kern_ms, lds_bytes_per_home, src):
             "assumption": "8 B x 64 lanes per LDS instruction (an upper estimate; most are b64)", "source": src}
     homes_per_cu = (160 * 1024) // max(1, lds_bytes_per_home)
     out["occupancy"] = {"lds_bytes_per_home": lds_bytes_per_home, "homes_per_cu_lds": homes_per_cu,
-                        "waves_per_simd": min(homes_per_cu / 4.0, 2.0),
-                        "limit": "LDS (one 64-lane workgroup per home) and 164 VGPRs: 2 waves per SIMD",
+                        "waves_per_simd": min(homes_per_cu / 4.0, 3.0),
+                        "limit": (f"LDS: {homes_per_cu} one-wave workgroups (homes) per CU; 168 VGPRs allow 3 waves "
+                                  "per SIMD (12 per CU)"),
                         "wait_share": (sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"] if "SQ_WAIT_ANY" in sq else None),
                         "issue_share": (sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"]
                                         if "SQ_ACTIVE_INST_ANY" in sq else None)}

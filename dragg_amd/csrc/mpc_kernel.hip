@@ -2828,7 +2828,7 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
 enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1 };
 
 template <bool EXPLICIT, int MODE>
-DEV void solve_direct(const KArgs& a, int home, double* smem, int slot) {
+DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int first_chain) {
     constexpr int NT = WAVE;
     const int lane = threadIdx.x;
     const int N = a.d.n_homes;
@@ -2892,7 +2892,9 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot) {
             if (lane == 0) list[atomicAdd(list + N, 1)] = home;
             return;
         }
-        for (int chain = 0; chain < 2 && ok; ++chain) {
+        // (the second launch resumes a home at the chain the hot launch deferred: the indoor-air
+        // chain's schedule is already in the global solution array when the tank chain deferred)
+        for (int chain = first_chain; chain < 2 && ok; ++chain) {
             reload_home(h, a, home, saved);
             twlo0 = saved[6]; twhi0 = saved[7];
             for (int k = lane; k < H; k += NT) {
@@ -2940,7 +2942,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot) {
             if (r >= 0) {
                 ok = r == 1;
             } else if (MODE == DM_FRONT) {                 // leave the home to DM_BUCKET
-                if (lane == 0) list[atomicAdd(list + N, 1)] = home;
+                if (lane == 0) list[atomicAdd(list + N, 1)] = home | (chain << 30);
                 return;
             } else {
                 ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
@@ -3015,7 +3017,7 @@ template <bool EXPLICIT, int MODE>
 __global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_kernel(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     if (MODE == DM_FRONT) {
-        if ((int)blockIdx.x < a.d.n_homes) solve_direct<EXPLICIT, MODE>(a, blockIdx.x, smem, 0);
+        if ((int)blockIdx.x < a.d.n_homes) solve_direct<EXPLICIT, MODE>(a, blockIdx.x, smem, 0, 0);
         return;
     }
     // persistent: block b solves the deferred homes b, b + gridDim.x, ... of the list (its own
@@ -3024,9 +3026,10 @@ __global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_ker
                                                          defer_offset(a.d.n_homes, a.d.horizon));
     const int cnt = min(list[a.d.n_homes], a.d.n_homes);
     for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
-        const int home = list[j];
-        if (home < 0 || home >= a.d.n_homes) continue;
-        solve_direct<EXPLICIT, MODE>(a, home, smem, blockIdx.x);
+        const int e = list[j];                      // home | deferred chain << 30
+        const int home = e & 0x3FFFFFFF, chain = (e >> 30) & 1;
+        if (home >= a.d.n_homes) continue;
+        solve_direct<EXPLICIT, MODE>(a, home, smem, blockIdx.x, chain);
         __syncthreads();
     }
 }
