@@ -39,7 +39,10 @@ constexpr int SECOND_SLOTS = 512;       // blocks of the persistent second launc
 constexpr int PRUNE_AT = 64;            // front size that switches on the LP-bound pruning
 constexpr int NF_HOT = 168;             // front capacity of the hot launch (front_layout): less LDS
                                         //   per home, more homes per CU; a larger front defers
-constexpr int NTB = 192;             // key buckets and cost buckets per stage (dp_front)
+constexpr int NTB_HOT = 128;          // key / cost buckets per stage of the hot launch's front DP
+                                      //   (small fronts; fewer buckets = less LDS = 12 homes per CU)
+constexpr int NTB = 192;              // ... of the second launch's regular front DP and round_lp
+constexpr int NTB_BIG = 256;          // ... of the big exact pass (fronts up to NF_BIG)
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
 
 constexpr double SIGMA = 1e-6;
@@ -1021,7 +1024,7 @@ DEV bool dp_chain(const Home& h, const Lds& L, const DpChain& c, int lane) {
     return true;
 }
 
-template <int SS, int CAP = NF, int CAPB = NF_BOUND, int PS = NB_CAP>
+template <int SS, int CAP = NF, int CAPB = NF_BOUND, int PS = NB_CAP, int NBK = NTB>
 DEV int dp_front(const struct FrontBufs& B, int H, int lane, double g, double x0, double lo0, double hi0, double lo,
                  double hi, int sx, int sv, bool use_bound = false, double ub_ext = INFINITY,
                  double* best_out = nullptr);
@@ -1462,10 +1465,10 @@ __host__ __device__ inline DirectLayout front_layout(int H) {
     o.lab = take(16 * NF_HOT, 16);
     o.rmin = take(16 * NF_HOT, 16);
     o.wl = take(8 * 3 * WAVE, 16);
-    o.kb = take(8 * NTB, 16);
-    o.cb = take(8 * NTB, 16);
-    o.mh = take(4 * NTB, 4);
-    o.kl = take(4 * NTB, 4);
+    o.kb = take(8 * NTB_HOT, 16);
+    o.cb = take(8 * NTB_HOT, 16);
+    o.mh = take(4 * NTB_HOT, 4);
+    o.kl = take(4 * NTB_HOT, 4);
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
     const int dp_end = p;
@@ -1538,10 +1541,10 @@ __host__ __device__ inline BigLayout big_layout(int H, int S) {
     o.fa = take(16 * NF_BIG, 16);
     o.fb = take(16 * NF_BIG, 16);
     o.wl = take(8 * 3 * WAVE, 16);
-    o.kb = take(8 * NTB, 16);
-    o.cb = take(8 * NTB, 16);
-    o.mh = take(4 * NTB, 4);
-    o.kl = take(4 * NTB, 4);
+    o.kb = take(8 * NTB_BIG, 16);
+    o.cb = take(8 * NTB_BIG, 16);
+    o.mh = take(4 * NTB_BIG, 4);
+    o.kl = take(4 * NTB_BIG, 4);
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
     o.bytes = (max(p, d.bytes) + 15) / 16 * 16;
@@ -2260,14 +2263,14 @@ DEV T dpp_iscan(T v, int lane, T id, Op op) {
     return row == 0 ? v : op(v, off);
 }
 
-template <int SS, int CAP, int CAPB, int PS>
+template <int SS, int CAP, int CAPB, int PS, int NBK>
 DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, double lo0, double hi0, double lo,
                  double hi, int sx, int sv, bool use_bound, double ub_ext, double* best_out) {
     static_assert(SS > 0 && SS < 16, "duty count must be a compile-time constant below 16");
     static_assert(CAP <= PS && CAPB <= PS && PS <= 4096, "back-pointer rows hold a 12-bit parent index");
     constexpr int NU = SS + 1;
-    constexpr int BPL = NTB / WAVE;      // buckets per lane in the scan
-    static_assert(NTB % WAVE == 0, "");
+    constexpr int BPL = NBK / WAVE;      // buckets per lane in the scan
+    static_assert(NBK % WAVE == 0, "");
     auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
     auto umin = [](unsigned a, unsigned b) { return a < b ? a : b; };
     auto umax = [](unsigned a, unsigned b) { return a > b ? a : b; };
@@ -2444,7 +2447,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     int n = 1;
     double xmin = x0, xmax = x0, cmin = 0.0, cmax = 0.0;    // state / cost range of the front
     const unsigned long long below = (1ull << lane) - 1ull;  // lanes < this one
-    for (int b = lane; b < NTB; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
+    for (int b = lane; b < NBK; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
     // W_{k+1} of the stage in the LDS table, W_{k+2} in flight
     double2 wnext = make_double2(INFINITY, INFINITY);
     if (prune) {
@@ -2478,7 +2481,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         }
         // the children's state and cost ranges (widened past rounding) define the two bucket
         // grids of this stage.  A child's position in a range as a 32-bit fixed-point number
-        // v = (key - lo) * NTB * 2^23 / (hi - lo) (one fma from the state) gives its bucket
+        // v = (key - lo) * NBK * 2^23 / (hi - lo) (one fma from the state) gives its bucket
         // (v >> 23) and, v being computed to far better than one unit, conservative bounds
         // v - 1 <= V <= v + 2 of the exact monotone position V: references use the bound that
         // understates them, the tested child the one that overstates it.
@@ -2488,9 +2491,9 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         xl -= tw(xl); xh += tw(xh);
         double clo = cmin + fmin(0.0, q * SS), chi = cmax + fmax(0.0, q * SS);
         clo -= tw(clo); chi += tw(chi);
-        // scales ~ NTB 2^23 / width by a refined reciprocal (any scale near it will do: the
+        // scales ~ NBK 2^23 / width by a refined reciprocal (any scale near it will do: the
         // positions are monotone and their bounds hold for the scale actually used)
-        const double FX = (double)NTB * 8388608.0;        // NTB * 2^23 <= 2^31
+        const double FX = (double)NBK * 8388608.0;        // NBK * 2^23 <= 2^31
         const double ksc = FX * rcp_nr(xh - xl), csc = FX * rcp_nr(chi - clo);
         // key position: (dx x - key_lo) * ksc with key_lo = dx > 0 ? xl : -xh
         const double kmul = dx * ksc, kadd = -(dx > 0.0 ? xl : -xh) * ksc;
@@ -2511,8 +2514,8 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             if (xc >= bl && xc <= bh && (!prune || cc + w_eval(B, xc) <= UBT)) {
                 const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
                 const unsigned cu = vc + 2u, kd = dn(vk);
-                atomicMin(&B.kb[min(NTB - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
-                atomicMax(&B.cb[min(NTB - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
+                atomicMin(&B.kb[min(NBK - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
+                atomicMax(&B.cb[min(NBK - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
             }
         }
         __syncthreads();
@@ -2567,7 +2570,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             bool keep = have && xc >= bl && xc <= bh;
             if (keep && prune) keep = cc + w_eval(B, xc) <= UBT;
             if (keep && !nodom) {
-                const int kbk = min(NTB - 1, (int)(vk >> 23)), cbk = min(NTB - 1, (int)(vc >> 23));
+                const int kbk = min(NBK - 1, (int)(vk >> 23)), cbk = min(NBK - 1, (int)(vc >> 23));
                 const unsigned ku = vk + 2u, cd = dn(vc);
                 const unsigned long long ky = B.kb[kbk], cy = B.cb[cbk];
                 const unsigned ycu = (unsigned)(ky >> 32), ykd = ~(unsigned)ky;
@@ -2611,7 +2614,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             cmin = c1 - tw(c1);
             cmax = c2 + tw(c2);
         }
-        for (int b = lane; b < NTB && !nodom; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
+        for (int b = lane; b < NBK && !nodom; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
         if (prune && k + 1 < H) {
             w_to_lds(B, lane, wnext.x, wnext.y);
             if (k + 3 <= H) wnext = load_row(k + 3);
@@ -2926,7 +2929,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 double* const wl = D.wl;
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
                                    wg, wl, wl + WAVE, wl + 2 * WAVE};
-                r = MODE == DM_FRONT ? dp_front<6, NF_HOT, NF_HOT>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound)
+                r = MODE == DM_FRONT ? dp_front<6, NF_HOT, NF_HOT, NB_CAP, NTB_HOT>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound)
                                      : dp_front<6, NF, NF_BOUND>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
 #ifdef DRAGG_FRONT_STATS2
                 // diagnostic: the T chain's fronts when the bound is the optimum itself
@@ -2970,7 +2973,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                                        D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE};
                     __syncthreads();
                     // keeps the bucketed schedule in D.x unless it finds (and writes) the optimum
-                    r2 = dp_front<6, NF_BIG, NF_BIG, NF_BIG>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
+                    r2 = dp_front<6, NF_BIG, NF_BIG, NF_BIG, NTB_BIG>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
                     if (r2 == 1) ok = true;
                     else if (r2 == 0 && !ok) ok = false;      // exact: no integer schedule
                     else if (r2 == 0) r2 = -4;                // bound inconsistent with the schedule: keep it
