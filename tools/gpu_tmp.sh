@@ -1,10 +1,7 @@
 set -o pipefail
-mkdir -p gpurun_out/s11
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rP --timeout 300 --timeout-method thread > gpurun_out/s11/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -60 gpurun_out/s11/pytest.log; exit 1; }
-tail -1 gpurun_out/s11/pytest.log
-timeout -k 10 200 python tools/count_paths.py 10000 12 96 7 2>&1 | grep -v amdgpu.ids || exit 1
-
-timeout -k 10 200 python tools/count_paths.py 10000 12 16 7 rl 2>&1 | grep -v amdgpu.ids || exit 1
-BENCH_ARGS="--steps 96 --homes 1250" bash tools/gpu_bench_ab.sh c14 c16 || exit 1
-BENCH_ARGS="--workload rl --steps 8" bash tools/gpu_bench_ab.sh c14 c16 || exit 1
-BENCH_ARGS="--steps 96" bash tools/gpu_bench_ab.sh c14 c16 || exit 1
+bash tools/gpu_final.sh || exit 1
+bash tools/gpu_profile.sh || exit 1
+cd /tmp && export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace1250 -o trace -- python3 bench.py --cpu-seconds 0 --homes 1250 > gpurun_out/prof/trace1250.log 2>&1 || exit 1
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/tracerl -o trace -- python3 bench.py --cpu-seconds 0 --workload rl --steps 8 > gpurun_out/prof/tracerl.log 2>&1 || exit 1
