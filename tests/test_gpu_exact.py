@@ -105,3 +105,54 @@ def test_integer_dp_is_exact(name, mode, gpu):
         # rounding level on these fixtures, round_lp's older fixed-grid dp_chain up to 1.4 %
         assert gaps.max() <= (1e-6 if mode == "round" else 0.02)
     print(msg)
+
+
+def test_wide_band_rl_price_second_launch_exact(gpu):
+    """Homes with a 20 C comfort band (wider than the bucketed DP's 352 moving buckets: its
+    fixed-grid branch `dp_fixed` runs) under a stage-varying RL price (the hot launch defers them;
+    the second launch's bucketed schedule bounds the exact big-front pass): every answer is still
+    the exact MILP optimum (oracle/thermal.py exact_milp), status for status."""
+    import math
+    import torch
+    from dragg_amd import _lib as L
+    from dragg_amd.community import synthetic_homes, synthetic_weather
+    from dragg_amd.mpc import MPCBatch
+    from oracle import mpc as M
+    from oracle import thermal as TH
+    hh, dt = 6, 4
+    homes = synthetic_homes(24, seed=77, days=2, dt=dt, horizon_hours=hh)
+    for h in homes:
+        h["hvac"]["temp_in_min"], h["hvac"]["temp_in_max"] = 12.0, 32.0
+        h["hvac"]["temp_in_init"] = 22.0
+    oat, ghi, tou = synthetic_weather(2, dt, 2, seed=78, month=7)
+    H = hh * dt
+    rp = [0.03 * math.cos(k / 3.0) for k in range(H)]
+    ins, opts = [], []
+    for h in homes:
+        hc = M.home_const(h)
+        draw, _, _ = M.water_draws(hc, 0)
+        T0, Tw0, E0, _ = M.initial_conditions(hc, 0, {}, draw)
+        o, g, tt = M.env_slice(oat, ghi, tou, 0, 0, H)
+        si = M.StepInput(t=0, T0=T0, Tw0=Tw0, E0=E0, oat=o, ghi=g, price=M.total_price(tt, rp, H), draw=draw,
+                         winter=False)
+        ins.append(si)
+        opts.append(TH.exact_milp(hc, si))
+    col = lambda k, n: np.array([np.asarray(getattr(s, k), float)[:n] for s in ins]).T  # noqa: E731
+    b = MPCBatch(homes, int_mode="round")
+    b.solve_explicit(t=np.zeros(len(homes), np.int32), T0=[s.T0 for s in ins], Tw0=[s.Tw0 for s in ins],
+                     E0=[np.nan if s.E0 is None else s.E0 for s in ins], counter=np.zeros(len(homes), np.int32),
+                     winter=np.zeros(len(homes), np.int32), draw=col("draw", H + 1), oat=col("oat", H + 1),
+                     ghi=col("ghi", H + 1), price=col("price", H))
+    torch.cuda.synchronize()
+    st, obj, path = b.status.cpu().numpy(), b.obj.cpu().numpy(), b.int_path.cpu().numpy()
+    n_opt = 0
+    for i, opt in enumerate(opts):
+        assert (st[i] == L.ST_OPTIMAL) == (opt is not None), (i, L.STATUS_NAMES[st[i]], opt)
+        assert path[i] & L.PATH_SECOND, (i, path[i])                 # solved by the second launch
+        if opt is None:
+            continue
+        n_opt += 1
+        assert path[i] & L.PATH_APPROX_MASK == 0, (i, path[i])
+        assert abs(obj[i] - opt) <= 1e-6 * max(1.0, abs(opt)), (i, obj[i], opt)
+    print(f"wide band + RL price: {n_opt} of {len(homes)} homes optimal, all equal to the exact optimum")
+    assert n_opt >= len(homes) // 2
