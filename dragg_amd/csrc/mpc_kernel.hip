@@ -2341,100 +2341,100 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         return lane < m ? B.wg[j * WAVE + lane] : make_double2(INFINITY, INFINITY);
     };
     auto make_bound = [&]() -> bool {
-    if (H >= 2 * WAVE) return false;                 // row counts held for 128 rows (a 32 h horizon)
-    bool prune = true;
-    {
-        double bl = H == 1 ? lo0 : lo, bh = H == 1 ? hi0 : hi;
-        bl -= tw(bl);
-        bh += tw(bh);
-        double wx = lane == 0 ? bl : lane == 1 ? bh : INFINITY, wv = lane < 2 ? 0.0 : INFINITY;
-        int m = 2;
-        if (lane < m) B.wg[H * WAVE + lane] = make_double2(wx, wv);
-        set_count(H, m);
-        for (int j = H - 1; j >= 1; --j) {
-            const double A = B.cA[j], C = B.cC[j], q = B.cq[j];
-            if (!(A > 0.0) || m + 1 > WAVE) { prune = false; break; }
-            const double zs = g * SS, cS = q * SS;
-            const double zlo = fmin(0.0, zs), zhi = fmax(0.0, zs);
-            const double cL = zs > 0.0 ? cS : 0.0, cR = zs > 0.0 ? 0.0 : cS;
-            const double F = lane < m ? fma(q * rcp_nr(g), wx, wv) : INFINITY;
-            const double Fm = dpp_reduce(F, [](double a, double b) { return fmin(a, b); });
-            const int js = __ffsll((long long)__ballot(F == Fm)) - 1;
-            const double px = __shfl_up(wx, 1), pv = __shfl_up(wv, 1);
-            const int m1 = m + 1;
-            const double iA = rcp_nr(A);
-            double nx = lane <= js ? wx - zhi : px - zlo;
-            double nv = lane <= js ? wv + cL : pv + cR;
-            nx = (nx - C) * iA;
-            if (lane >= m1) { nx = INFINITY; nv = INFINITY; }
-            double cl = j == 1 ? lo0 : lo, ch = j == 1 ? hi0 : hi;
-            cl -= tw(cl);
-            ch += tw(ch);
-            const double dl = fmax(cl, read_lane(nx, 0)), dh = fmin(ch, read_lane(nx, m1 - 1));
-            if (!(dl <= dh)) { prune = false; break; }
-            const double vdl = pl_eval(nx, nv, m1, dl), vdh = pl_eval(nx, nv, m1, dh);
-            const bool in = lane < m1 && nx > dl && nx < dh;
-            const unsigned long long bal = __ballot(in);
-            const int m2 = __popcll(bal) + 2;
-            if (m2 > WAVE) { prune = false; break; }
-            // compact through the LDS table (free here)
-            if (in) {
-                const int pos_ = 1 + __popcll(bal & ((1ull << lane) - 1ull));
-                B.wlx[pos_] = nx;
-                B.wlv[pos_] = nv;
-            }
-            if (lane == 0) {
-                B.wlx[0] = dl; B.wlv[0] = vdl;
-                B.wlx[m2 - 1] = dh; B.wlv[m2 - 1] = vdh;
-            }
-            __syncthreads();
-            wx = lane < m2 ? B.wlx[lane] : INFINITY;
-            wv = lane < m2 ? B.wlv[lane] : INFINITY;
-            m = m2;
-            __syncthreads();
-            if (lane < m) B.wg[j * WAVE + lane] = make_double2(wx, wv);
-            set_count(j, m);
-        }
-    }
-    // (d) an upper bound: the cost of one feasible schedule, greedy in q u + W_{k+1}(x') (the
-    //     labels' own arithmetic).  Children with cost + W > bound (+ a margin past rounding)
-    //     cannot lead to the optimum and are dropped.
-    if (prune) {
-        double qabs = 0.0;
-        for (int k = lane; k < H; k += WAVE) qabs += fabs(B.cq[k]) * SS;
-        qabs = dpp_sum(qabs);
-        double gx = x0, ub = 0.0;
-        bool gok = true;
-        double2 cur = load_row(1);
-        for (int k = 0; k < H && gok; ++k) {
-            double2 nxt = k + 2 <= H ? load_row(k + 2) : make_double2(INFINITY, INFINITY);
-            w_to_lds(B, lane, cur.x, cur.y);
-            __syncthreads();
-            const double A = B.cA[k], C = B.cC[k], q = B.cq[k];
-            double bl = k == 0 ? lo0 : lo, bh = k == 0 ? hi0 : hi;
+        if (H >= 2 * WAVE) return false;                 // row counts held for 128 rows (a 32 h horizon)
+        bool prune = true;
+        {
+            double bl = H == 1 ? lo0 : lo, bh = H == 1 ? hi0 : hi;
             bl -= tw(bl);
             bh += tw(bh);
-            if (k + 1 < H) {
-                bl = fmax(bl, fma((double)B.flo[k + 1], hs, hb));
-                bh = fmin(bh, fma((double)B.fhi[k + 1], hs, hb));
+            double wx = lane == 0 ? bl : lane == 1 ? bh : INFINITY, wv = lane < 2 ? 0.0 : INFINITY;
+            int m = 2;
+            if (lane < m) B.wg[H * WAVE + lane] = make_double2(wx, wv);
+            set_count(H, m);
+            for (int j = H - 1; j >= 1; --j) {
+                const double A = B.cA[j], C = B.cC[j], q = B.cq[j];
+                if (!(A > 0.0) || m + 1 > WAVE) { prune = false; break; }
+                const double zs = g * SS, cS = q * SS;
+                const double zlo = fmin(0.0, zs), zhi = fmax(0.0, zs);
+                const double cL = zs > 0.0 ? cS : 0.0, cR = zs > 0.0 ? 0.0 : cS;
+                const double F = lane < m ? fma(q * rcp_nr(g), wx, wv) : INFINITY;
+                const double Fm = dpp_reduce(F, [](double a, double b) { return fmin(a, b); });
+                const int js = __ffsll((long long)__ballot(F == Fm)) - 1;
+                const double px = __shfl_up(wx, 1), pv = __shfl_up(wv, 1);
+                const int m1 = m + 1;
+                const double iA = rcp_nr(A);
+                double nx = lane <= js ? wx - zhi : px - zlo;
+                double nv = lane <= js ? wv + cL : pv + cR;
+                nx = (nx - C) * iA;
+                if (lane >= m1) { nx = INFINITY; nv = INFINITY; }
+                double cl = j == 1 ? lo0 : lo, ch = j == 1 ? hi0 : hi;
+                cl -= tw(cl);
+                ch += tw(ch);
+                const double dl = fmax(cl, read_lane(nx, 0)), dh = fmin(ch, read_lane(nx, m1 - 1));
+                if (!(dl <= dh)) { prune = false; break; }
+                const double vdl = pl_eval(nx, nv, m1, dl), vdh = pl_eval(nx, nv, m1, dh);
+                const bool in = lane < m1 && nx > dl && nx < dh;
+                const unsigned long long bal = __ballot(in);
+                const int m2 = __popcll(bal) + 2;
+                if (m2 > WAVE) { prune = false; break; }
+                // compact through the LDS table (free here)
+                if (in) {
+                    const int pos_ = 1 + __popcll(bal & ((1ull << lane) - 1ull));
+                    B.wlx[pos_] = nx;
+                    B.wlv[pos_] = nv;
+                }
+                if (lane == 0) {
+                    B.wlx[0] = dl; B.wlv[0] = vdl;
+                    B.wlx[m2 - 1] = dh; B.wlv[m2 - 1] = vdh;
+                }
+                __syncthreads();
+                wx = lane < m2 ? B.wlx[lane] : INFINITY;
+                wv = lane < m2 ? B.wlv[lane] : INFINITY;
+                m = m2;
+                __syncthreads();
+                if (lane < m) B.wg[j * WAVE + lane] = make_double2(wx, wv);
+                set_count(j, m);
             }
-            const double xc = fma(A, gx, fma(g, (double)lane, C));
-            double val = INFINITY;
-            if (lane <= SS && xc >= bl && xc <= bh) val = (double)lane * q + w_eval(B, xc);
-            const double vm = dpp_reduce(val, [](double a, double b) { return fmin(a, b); });
-            if (!(vm < INFINITY)) { gok = false; break; }
-            const int bu = __ffsll((long long)__ballot(val == vm)) - 1;
-            gx = read_lane(xc, bu);
-            ub = fma(q, (double)bu, ub);
-            cur = nxt;
-            __syncthreads();
         }
-        if (gok) UBT = ub + TOL_P * (1.0 + fabs(ub) + qabs);
-        // a caller's upper bound (the cost of a schedule it already has), with the same margin
-        if (ub_ext < INFINITY) { UBT = fmin(UBT, ub_ext + TOL_P * (1.0 + fabs(ub_ext) + qabs)); gok = true; }
-        if (!gok) prune = false;
-    }
-    return prune;
+        // (d) an upper bound: the cost of one feasible schedule, greedy in q u + W_{k+1}(x') (the
+        //     labels' own arithmetic).  Children with cost + W > bound (+ a margin past rounding)
+        //     cannot lead to the optimum and are dropped.
+        if (prune) {
+            double qabs = 0.0;
+            for (int k = lane; k < H; k += WAVE) qabs += fabs(B.cq[k]) * SS;
+            qabs = dpp_sum(qabs);
+            double gx = x0, ub = 0.0;
+            bool gok = true;
+            double2 cur = load_row(1);
+            for (int k = 0; k < H && gok; ++k) {
+                double2 nxt = k + 2 <= H ? load_row(k + 2) : make_double2(INFINITY, INFINITY);
+                w_to_lds(B, lane, cur.x, cur.y);
+                __syncthreads();
+                const double A = B.cA[k], C = B.cC[k], q = B.cq[k];
+                double bl = k == 0 ? lo0 : lo, bh = k == 0 ? hi0 : hi;
+                bl -= tw(bl);
+                bh += tw(bh);
+                if (k + 1 < H) {
+                    bl = fmax(bl, fma((double)B.flo[k + 1], hs, hb));
+                    bh = fmin(bh, fma((double)B.fhi[k + 1], hs, hb));
+                }
+                const double xc = fma(A, gx, fma(g, (double)lane, C));
+                double val = INFINITY;
+                if (lane <= SS && xc >= bl && xc <= bh) val = (double)lane * q + w_eval(B, xc);
+                const double vm = dpp_reduce(val, [](double a, double b) { return fmin(a, b); });
+                if (!(vm < INFINITY)) { gok = false; break; }
+                const int bu = __ffsll((long long)__ballot(val == vm)) - 1;
+                gx = read_lane(xc, bu);
+                ub = fma(q, (double)bu, ub);
+                cur = nxt;
+                __syncthreads();
+            }
+            if (gok) UBT = ub + TOL_P * (1.0 + fabs(ub) + qabs);
+            // a caller's upper bound (the cost of a schedule it already has), with the same margin
+            if (ub_ext < INFINITY) { UBT = fmin(UBT, ub_ext + TOL_P * (1.0 + fabs(ub_ext) + qabs)); gok = true; }
+            if (!gok) prune = false;
+        }
+        return prune;
     };
     bool prune = B.wg != nullptr && (use_bound || nodom) && make_bound();
     if (nodom && !prune) return nodom && (pos && neg) ? -1 : -2;
@@ -2592,7 +2592,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             }
         }
 #ifdef DRAGG_FRONT_STATS
-        if (lane == 0) B.x[k * 8 + S_PAD] += (double)nn * (B.x[sx] == -12345.0 ? 1.0 : 1.0) * (sx == S_T ? 1.0 : 1e4) +
+        if (lane == 0) B.x[k * 8 + S_PAD] += (double)nn * (sx == S_T ? 1.0 : 1e4) +
                                              (k == 0 ? (prune ? 1e8 : 0.0) * (sx == S_T ? 1.0 : 2.0) : 0.0);
 #endif
         if (nn == 0) return 0;                       // no child left inside the feasible set
