@@ -52,7 +52,40 @@ def parse():
                          "is one RL reward-price action: price broadcast, --forecast-horizon rollout "
                          "re-solves of the community, the committed step, the sums to the host")
     ap.add_argument("--forecast-horizon", type=int, default=1, help="rl: rollout timesteps per action")
+    ap.add_argument("--keep-crashing-homes", action="store_true",
+                    help="keep battery homes whose t = 0 solve fails (the reference raises KeyError at t = 1)")
     return ap.parse_args()
+
+
+def reference_completable(homes, oat, ghi, tou, rounds=8):
+    """A community the reference completes.  A battery home whose t = 0 solve fails leaves no
+    e_batt_opt in its hash, and the reference raises KeyError('e_batt_opt') at t = 1
+    (mpc_calc.py:280-289).  The failures come from the season draw (keyed by the home's index:
+    a "winter" draw on a hot day leaves the cooling duty at zero), not from the home's
+    parameters, so each such battery home swaps places with a home without a battery (whose
+    failed t = 0 solve the reference survives) until the t = 0 step solves every battery home.
+    Deterministic: every rank builds the same community.  -> (homes, swaps)"""
+    import torch
+    from dragg_amd import _lib as L
+    from dragg_amd.mpc import MPCBatch
+    homes, swaps = list(homes), 0
+    donors = [j for j in range(len(homes) - 1, -1, -1) if "battery" not in homes[j]["type"]]
+    for _ in range(rounds):
+        b = MPCBatch(homes, oat, ghi, tou, 0, [0.0], int_mode="round", seed=12)
+        b.step(0)
+        st = b.status.cpu().numpy()
+        del b
+        torch.cuda.empty_cache()
+        bad = [i for i, h in enumerate(homes) if "battery" in h["type"] and st[i] != L.ST_OPTIMAL]
+        if not bad or not donors:
+            break
+        for i in bad:
+            if not donors:
+                break
+            j = donors.pop(0)
+            homes[i], homes[j] = homes[j], homes[i]
+            swaps += 1
+    return homes, swaps
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -240,6 +273,10 @@ def main():
     if backend != "nccl":
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
+    # (after the CPU leg: its worker processes fork before anything touches the GPU)
+    replaced = None
+    if not args.keep_crashing_homes:
+        homes, replaced = reference_completable(homes, oat, ghi, tou)
     if world > 1:
         if backend == "nccl":
             torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -322,6 +359,11 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (NSRDB-shaped weather, config.toml-range homes, seeded)",
+            "community": {"battery_home_swaps": replaced,
+                          "note": "battery homes whose t = 0 solve fails (the reference raises KeyError at "
+                                  "t = 1, mpc_calc.py:280-289; the failure follows the index-keyed season "
+                                  "draw) swapped with homes without a battery, so the run is one the "
+                                  "reference completes; null = kept (--keep-crashing-homes)"},
             "config": {"workload": workload, "baseline_config": "BASELINE.json configs[4]" if rl else "BASELINE.json configs[2]",
                        "homes_total": n_total, "homes_per_gpu": agg.batch.N, "global_batch": n_total,
                        "horizon": H, "mix": "40/20/20/20 base/pv/battery/pv_battery",

@@ -6,6 +6,7 @@ import subprocess
 import sys
 
 name, spec = sys.argv[1], sys.argv[2]
+SCHED = ["-mllvm", "-amdgpu-sched-strategy=" + (sys.argv[3] if len(sys.argv) > 3 else "iterative-ilp")]
 R = runpy.run_path(spec)["R"]
 src = open("dragg_amd/csrc/mpc_kernel.hip").read()
 for o, n in R:
@@ -15,7 +16,7 @@ tmp = f"dragg_amd/csrc/_var_{name}.hip"
 open(tmp, "w").write(src)
 os.makedirs("varlib", exist_ok=True)
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wno-unused-function",
-       "-Wno-unused-variable", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp", "-o", f"varlib/{name}.so", tmp]
+       "-Wno-unused-variable", *SCHED, "-o", f"varlib/{name}.so", tmp]
 r = subprocess.run(cmd, capture_output=True, text=True)
 os.remove(tmp)
 print(r.stderr[-2000:] if r.returncode else f"varlib/{name}.so")
