@@ -39,8 +39,8 @@ constexpr int SECOND_SLOTS = 512;       // blocks of the persistent second launc
 constexpr int PRUNE_AT = 64;            // front size that switches on the LP-bound pruning
 constexpr int NF_HOT = 168;             // front capacity of the hot launch (front_layout): less LDS
                                         //   per home, more homes per CU; a larger front defers
-constexpr int NTB_HOT = 128;          // key / cost buckets per stage of the hot launch's front DP
-                                      //   (small fronts; fewer buckets = less LDS = 12 homes per CU)
+constexpr int NTB_HOT = 64;           // key / cost buckets per stage of the hot launch's front DP
+                                      //   (small fronts: a one-bucket-per-lane scan; measured 128: +6 % time)
 constexpr int NTB = 192;              // ... of the second launch's regular front DP and round_lp
 constexpr int NTB_BIG = 256;          // ... of the big exact pass (fronts up to NF_BIG)
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };

@@ -1,7 +1,8 @@
 set -o pipefail
-mkdir -p gpurun_out/s15
-timeout -k 10 200 python -u bench.py --cpu-seconds 0 --homes 1000 --horizon-hours 6 --month 1 > gpurun_out/s15/cfg1.log 2>&1 || exit 1
-timeout -k 10 200 python -u bench.py --cpu-seconds 0 --homes 10000 --horizon-hours 6 > gpurun_out/s15/h24.log 2>&1 || exit 1
-timeout -k 10 300 python -u bench.py --homes 100000 --horizon-hours 6 --steps 24 --cpu-seconds 0 > gpurun_out/s15/100k.log 2>&1 || exit 1
-timeout -k 10 200 python -u bench.py --cpu-seconds 0 --steps 48 > gpurun_out/s15/bench.log 2>&1 || exit 1
-for f in cfg1 h24 100k bench; do tail -1 gpurun_out/s15/$f.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]), d["ms_per_step"], d["status_counts"], d["community"]["battery_home_swaps"])'; done
+bash tools/gpu_final.sh || exit 1
+bash tools/gpu_profile.sh || exit 1
+cd /tmp && export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace1250 -o trace -- python3 bench.py --cpu-seconds 0 --homes 1250 > gpurun_out/prof/trace1250.log 2>&1 || exit 1
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/tracerl -o trace -- python3 bench.py --cpu-seconds 0 --workload rl --steps 8 > gpurun_out/prof/tracerl.log 2>&1 || exit 1
+timeout -k 10 200 python tools/count_paths.py 10000 12 16 7 rl 2>&1 | grep -v amdgpu.ids || exit 1
