@@ -22,7 +22,6 @@ only): the repo's CPU restatement of the reference solve (oracle/, HiGHS MILP in
 GLPK_MI) timed on this host's cores on a bounded sample of the same workload.
 """
 import argparse
-import ctypes
 import json
 import math
 import os
@@ -33,7 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=96)
@@ -43,69 +42,92 @@ def parse():
     ap.add_argument("--dt", type=int, default=4)
     ap.add_argument("--month", type=int, default=7, choices=[1, 4, 7, 10])
     ap.add_argument("--int-mode", default="round", choices=["round", "relax", "round_lp"])
-    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (0 = skip)")
-    ap.add_argument("--cpu-workers", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=60.0,
+                    help="CPU baseline wall budget (0 = skip; with --cpu-only, 0 = no limit)")
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0 = the host cores this job may use")
     ap.add_argument("--cpu-home-steps", type=int, default=1000,
-                    help="CPU baseline sample size (home-steps; stopped at --cpu-seconds of wall time)")
+                    help="CPU baseline sample size (home-steps; stopped early at --cpu-seconds of wall time)")
+    ap.add_argument("--cpu-milp-limit", type=float, default=300.0,
+                    help="HiGHS time limit per CPU solve; solves that reach it are counted separately")
+    ap.add_argument("--cpu-only", action="store_true",
+                    help="run only the CPU baseline (no GPU) and print its JSON (the committed full run)")
     ap.add_argument("--workload", default="rbo", choices=["rbo", "rl"],
                     help="rbo: run_rbo_mpc closed loop (configs[2], default); rl: configs[4], every step "
                          "is one RL reward-price action: price broadcast, --forecast-horizon rollout "
                          "re-solves of the community, the committed step, the sums to the host")
     ap.add_argument("--forecast-horizon", type=int, default=1, help="rl: rollout timesteps per action")
+    ap.add_argument("--rl-price", default="smooth", choices=["smooth", "flat"],
+                    help="rl: the agent's reward price per action: 'smooth' varies over the horizon "
+                         "(-0.03 cos(k/3) + a per-action offset, the shape of test_gpu_configs.py's "
+                         "configs[4] test: the price changes at every stage); 'flat' "
+                         "is one constant per action (round 2's RL line)")
+    ap.add_argument("--no-history", action="store_true",
+                    help="skip the per-step history write (collected_data); a configs[2] run keeps it")
     ap.add_argument("--keep-crashing-homes", action="store_true",
                     help="keep battery homes whose t = 0 solve fails (the reference raises KeyError at t = 1)")
-    return ap.parse_args()
-
-
-def reference_completable(homes, oat, ghi, tou, rounds=8):
-    """A community the reference completes.  A battery home whose t = 0 solve fails leaves no
-    e_batt_opt in its hash, and the reference raises KeyError('e_batt_opt') at t = 1
-    (mpc_calc.py:280-289).  The failures come from the season draw (keyed by the home's index:
-    a "winter" draw on a hot day leaves the cooling duty at zero), not from the home's
-    parameters, so each such battery home swaps places with a home without a battery (whose
-    failed t = 0 solve the reference survives) until the t = 0 step solves every battery home.
-    Deterministic: every rank builds the same community.  -> (homes, swaps)"""
-    import torch
-    from dragg_amd import _lib as L
-    from dragg_amd.mpc import MPCBatch
-    homes, swaps = list(homes), 0
-    donors = [j for j in range(len(homes) - 1, -1, -1) if "battery" not in homes[j]["type"]]
-    for _ in range(rounds):
-        b = MPCBatch(homes, oat, ghi, tou, 0, [0.0], int_mode="round", seed=12)
-        b.step(0)
-        st = b.status.cpu().numpy()
-        del b
-        torch.cuda.empty_cache()
-        bad = [i for i, h in enumerate(homes) if "battery" in h["type"] and st[i] != L.ST_OPTIMAL]
-        if not bad or not donors:
-            break
-        for i in bad:
-            if not donors:
-                break
-            j = donors.pop(0)
-            homes[i], homes[j] = homes[j], homes[i]
-            swaps += 1
-    return homes, swaps
+    return ap.parse_args(argv)
 
 
 # ----------------------------------------------------------------------------- CPU baseline
+def host_cores():
+    """The host cores this job may use: the affinity mask, the cgroup CPU quota and the job's
+    worker cap (MAX_JOBS: the GPU box grants one GPU's job a share of the host's cores and sets it
+    to that share) -- the smallest of them, and each of them for the record."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = float(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = float(f.read())
+            quota = q / per if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    cap = int(os.environ["MAX_JOBS"]) if os.environ.get("MAX_JOBS", "").isdigit() else None
+    n = min(x for x in (aff, math.ceil(quota) if quota else None, cap) if x)
+    return max(1, n), {"affinity": aff, "cgroup_quota": quota, "max_jobs": cap, "os_cpu_count": os.cpu_count()}
+
+
 def _cpu_worker(args):
-    """Closed-loop oracle solves of a few homes (t = 0, 1, ...), each solve a HiGHS MILP to the
-    reference's stopping rule, until the deadline or the home-step quota (runs before any GPU use)."""
+    """Closed-loop oracle solves of a few homes (t = 0, 1, ...), each the reference's MILP solved by
+    HiGHS, until the deadline or the home-step quota (runs before any GPU use).
+    -> (home-steps, per-solve seconds, solves that reached the time limit)"""
     homes, env, deadline, milp_limit, steps_per_home, quota = args
     from oracle import mpc as M
+    from scipy.optimize import milp, LinearConstraint, Bounds
     import numpy as np
-    n, times = 0, []
+    n, times, limited = 0, [], [0]
+
+    def solver(P):
+        """solve_problem's HiGHS call, recording whether the time limit cut it (HiGHS status 1)"""
+        # the per-solve limit, cut to what is left of the sample's wall budget (a solve in flight
+        # at the deadline ends there with its incumbent and is counted as time-limited)
+        lim = milp_limit if not deadline else max(1.0, min(milp_limit, deadline - time.time()))
+        res = milp(P["c"], constraints=[LinearConstraint(P["A_eq"], P["b_eq"], P["b_eq"]),
+                                        LinearConstraint(P["A_ub"], -np.inf, P["b_ub"])],
+                   integrality=P["integrality"], bounds=Bounds(-np.inf, np.inf),
+                   options={"time_limit": lim, "mip_rel_gap": 1e-6, "presolve": True})
+        if res.status == 1:
+            limited[0] += 1
+        if res.x is None:
+            return ({2: "infeasible", 3: "unbounded"}.get(res.status, "solver_error"), None, None)
+        x = res.x.copy()
+        ii = P["integrality"] == 1
+        x[ii] = np.floor(x[ii] + 0.5)
+        return "optimal", x, float(P["c"] @ x)
     for home in homes:
         hc = M.home_const(home)
         hsh = {}
         rng = np.random.default_rng(1234)
-
-        def solver(P):
-            return M.solve_problem(P, integer=True, time_limit=milp_limit)
         for t in range(steps_per_home):
-            if time.time() >= deadline or n >= quota:
-                return n, times
+            if (deadline and time.time() >= deadline) or n >= quota:
+                return n, times, limited[0]
             t0 = time.time()
             try:
                 M.run_home_step(hc, t, hsh, env, rng.standard_normal(hc.H), solver=solver)
@@ -113,21 +135,21 @@ def _cpu_worker(args):
                 break
             times.append(time.time() - t0)
             n += 1
-    return n, times
+    return n, times, limited[0]
 
 
-def cpu_baseline(homes, env, seconds, workers, home_steps, steps_per_home=4):
-    """The reference's per-home solve restated on the host (oracle/mpc.py: the reference's
-    problem build, HiGHS MILP standing in for GLPK_MI, cleanup/fallback), one process per worker,
-    on a sample of this workload's home-steps: `home_steps` of them (homes spread over the
-    community, steps_per_home closed-loop steps each), stopped at `seconds` of wall time.  The
-    rate is extrapolated to the whole workload (solves are independent across homes)."""
+def cpu_baseline(homes, env, seconds, workers, home_steps, milp_limit=300.0, steps_per_home=4):
+    """The reference's per-home solve restated on the host (oracle/mpc.py: the reference's problem
+    build, HiGHS MILP standing in for GLPK_MI, cleanup/fallback), one process per host core this
+    job may use (one process per core), on `home_steps` home-steps of this workload
+    (homes spread over the community, steps_per_home closed-loop steps each from t = 0), stopped
+    early at `seconds` of wall time (0: no limit).  The rate is extrapolated to the whole workload
+    (solves are independent across homes)."""
     import multiprocessing as mp
     import numpy as np
-    cores = len(os.sched_getaffinity(0))
-    workers = workers or max(1, min(16, cores))
-    milp_limit = 10.0
-    deadline = time.time() + seconds
+    cores, info = host_cores()
+    workers = workers or cores
+    deadline = time.time() + seconds if seconds > 0 else 0.0
     n_homes = max(workers, -(-home_steps // steps_per_home))
     picks = [homes[(i * 7919) % len(homes)] for i in range(n_homes)]
     per = [picks[w::workers] for w in range(workers)]
@@ -138,14 +160,36 @@ def cpu_baseline(homes, env, seconds, workers, home_steps, steps_per_home=4):
     wall = time.time() - t0
     n = sum(r[0] for r in res)
     times = [x for r in res for x in r[1]]
-    return {"value": n / wall if wall > 0 else 0.0, "unit": "solves/s", "cores": workers, "host_cores": cores,
-            "kind": "port", "home_steps": n, "extrapolated": True,
+    limited = sum(r[2] for r in res)
+    return {"value": n / wall if wall > 0 else 0.0, "unit": "solves/s", "cores": workers, "host_cores": info,
+            "kind": "port", "home_steps": n, "target_home_steps": home_steps, "time_limited_solves": limited,
+            "extrapolated": True, "wall_s": wall,
+            "median_solve_s": float(np.median(times)) if times else None,
+            "mean_solve_s": float(np.mean(times)) if times else None,
             "sample": f"{n} home-steps of this workload ({len(picks)} homes spread over the community, up to "
-                      f"{steps_per_home} closed-loop steps each from t = 0, {workers} worker processes on "
-                      f"{cores} host cores) solved by oracle/mpc.py (the reference's problem build, HiGHS MILP in "
-                      f"place of GLPK_MI, time_limit {milp_limit:.0f}s/solve) in {wall:.1f}s wall; median "
-                      f"{np.median(times) if times else float('nan'):.2f}s per solve; the rate is extrapolated to "
-                      f"the whole workload (home solves are independent)"}
+                      f"{steps_per_home} closed-loop steps each from t = 0) on {workers} worker processes, one per "
+                      f"host core this job may use (affinity {info['affinity']}, cgroup quota {info['cgroup_quota']}, "
+                      f"MAX_JOBS {info['max_jobs']}), solved by oracle/mpc.py (the reference's problem build, "
+                      f"HiGHS MILP with mip_rel_gap 1e-6 in place of GLPK_MI, time limit {milp_limit:.0f} s per "
+                      f"solve, cut to the sample's remaining wall budget: {limited} solves reached a limit and "
+                      f"count with their incumbent, so the rate is if anything overstated) in {wall:.1f} s wall; "
+                      f"median {np.median(times) if times else float('nan'):.2f} s per solve; extrapolated to the "
+                      f"whole workload (home solves are independent)"}
+
+
+def committed_cpu_baseline():
+    """The committed full CPU-baseline run (bench.py --cpu-only on the GPU box, >= 1,000
+    home-steps): profiles/*/cpu_baseline_full.json, newest first."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "cpu_baseline_full.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        return {k: d.get(k) for k in ("value", "unit", "cores", "home_steps", "time_limited_solves",
+                                     "median_solve_s", "wall_s", "workload")} | {"source": os.path.relpath(f, ROOT)}
+    return None
 
 
 # ----------------------------------------------------------------------------- roofline
@@ -165,11 +209,13 @@ def bytes_per_launch(batch, success_frac):
 
 
 def measured_pmc(workload_key):
-    """The committed rocprofv3 PMC passes of this workload (profiles/*/traffic.json): HBM
-    bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) and the SQ
-    counters per launch."""
+    """The committed rocprofv3 passes of EXACTLY this command's workload and timed window
+    (profiles/*/traffic.json, written by tools/make_traffic.py from the kernel trace and the PMC
+    passes of the same bench command): HBM bytes per step (FETCH_SIZE x 2 + WRITE_SIZE,
+    MI355X_MICROARCH.md HBM section), SQ counters per step and the profiled kernel time per
+    step, all over the timed steps only."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic*.json")), reverse=True):
         try:
             with open(f) as fh:
                 tj = json.load(fh)
@@ -195,21 +241,25 @@ def valu_cycles(sq):
     return 2.0 * (sq["SQ_INSTS_VALU"] - f64 - trans) + 4.0 * f64 + 8.0 * trans
 
 
-def extra_rooflines(pmc, kern_ms, lds_bytes_per_home, src):
-    """The bounds that do limit the kernel, from the committed PMC passes of
-    this workload (per solver step) and the step's kernel time measured in this run."""
-    sq = pmc.get("sq_per_launch", {})
-    if "SQ_INSTS_VALU" not in sq:
+def extra_rooflines(pmc, src):
+    """The bounds that do limit the kernel, from the committed profile of
+    this very command (counters per step over the timed steps, divided by the kernel time per step
+    of the SAME profiled run, so each number recomputes from profiles/).  Without such a profile:
+    none (no borrowed or window-mismatched counters)."""
+    sq = pmc.get("sq_per_step", {})
+    ks_ms = pmc.get("kernel_ms_per_step")
+    if "SQ_INSTS_VALU" not in sq or not ks_ms:
         return {}
-    ks = kern_ms * 1e-3
+    ks = ks_ms * 1e-3
     out = {}
     if "SQ_INSTS_VALU_FMA_F64" in sq:
         cyc = valu_cycles(sq)
         out["roofline_valu"] = {
             "bound": "valu-issue", "achieved": cyc / ks / 1e12, "peak": N_SIMD * CLOCK / 1e12,
             "unit": "T SIMD-cycles/s", "frac": cyc / ks / (N_SIMD * CLOCK),
-            "valu_per_launch": sq["SQ_INSTS_VALU"],
-            "fp64_valu_per_launch": sum(sq.get(f"SQ_INSTS_VALU_{c}_F64", 0) for c in ("ADD", "MUL", "FMA", "TRANS")),
+            "valu_per_step": sq["SQ_INSTS_VALU"],
+            "fp64_valu_per_step": sum(sq.get(f"SQ_INSTS_VALU_{c}_F64", 0) for c in ("ADD", "MUL", "FMA", "TRANS")),
+            "profiled_kernel_ms_per_step": ks_ms,
             "model": "2 cycles per wave64 VALU instruction, 4 per fp64 add/mul/fma, 8 per fp64 transcendental",
             "source": src}
     if "SQ_ACTIVE_INST_VALU" in sq and "SQ_WAVE_CYCLES" in sq:
@@ -219,31 +269,70 @@ def extra_rooflines(pmc, kern_ms, lds_bytes_per_home, src):
         b = sq["SQ_INSTS_LDS"] * 64 * 8
         out["roofline_lds"] = {
             "bound": "lds", "achieved": b / ks / 1e12, "peak": LDS_PEAK_TBS, "unit": "TB/s",
-            "frac": b / ks / 1e12 / LDS_PEAK_TBS, "lds_instr_per_launch": sq["SQ_INSTS_LDS"],
+            "frac": b / ks / 1e12 / LDS_PEAK_TBS, "lds_instr_per_step": sq["SQ_INSTS_LDS"],
             "bank_conflict_share": (sq["SQ_LDS_BANK_CONFLICT"] / sq["SQ_LDS_IDX_ACTIVE"]
                                     if sq.get("SQ_LDS_IDX_ACTIVE") else None),
+            "profiled_kernel_ms_per_step": ks_ms,
             "assumption": "8 B x 64 lanes per LDS instruction (an upper estimate; most are b64)", "source": src}
-    homes_per_cu = (160 * 1024) // max(1, lds_bytes_per_home)
-    out["occupancy"] = {"lds_bytes_per_home": lds_bytes_per_home, "homes_per_cu_lds": homes_per_cu,
-                        "waves_per_simd": min(homes_per_cu / 4.0, 3.0),
-                        "limit": (f"LDS: {homes_per_cu} one-wave workgroups (homes) per CU; 168 VGPRs allow 3 waves "
-                                  "per SIMD (12 per CU)"),
-                        "wait_share": (sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"] if "SQ_WAIT_ANY" in sq else None),
-                        "issue_share": (sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"]
-                                        if "SQ_ACTIVE_INST_ANY" in sq else None)}
+    if "SQ_WAIT_ANY" in sq and "SQ_WAVE_CYCLES" in sq:
+        out["wave_cycle_shares"] = {"wait_any": sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"],
+                                    "issue_any": (sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"]
+                                                  if "SQ_ACTIVE_INST_ANY" in sq else None), "source": src}
     fs = pmc.get("front_stats")
-    if fs:
-        out["dp_work"] = {"unit": "G label relaxations/s", "achieved": fs["children_per_launch"] / ks / 1e9,
-                          "children_per_launch": fs["children_per_launch"],
+    if fs and fs.get("children_per_step"):
+        out["dp_work"] = {"unit": "G label relaxations/s", "achieved": fs["children_per_step"] / ks / 1e9,
+                          "children_per_step": fs["children_per_step"],
                           "front_mean": [fs["front_mean_T"], fs["front_mean_W"]],
+                          "profiled_kernel_ms_per_step": ks_ms,
                           "definition": "one label relaxation = one child (parent label, duty) of a front DP stage: "
                                         "state and cost update, box test, bucket positions, dominance tests",
                           "source": src}
     return out
 
 
-def traffic_key(n_total, H, dt, month, int_mode, world):
-    return f"{n_total} homes, H={H}, dt={dt}, month {month}, int_mode={int_mode}, {world} rank(s)"
+def occupancy(batch):
+    """Registers, spills, LDS and resident homes per CU of the step's launches, as the code object
+    and the runtime report them on this device (dragg_mpc_kernel_info_get)."""
+    from dragg_amd import _lib as L
+    hot, second = L.kernel_info(batch.dims)
+    return {"hot": hot | {"waves_per_simd": hot["blocks_per_cu"] / 4.0},
+            "second": second,
+            "source": "hipFuncGetAttributes + hipOccupancyMaxActiveBlocksPerMultiprocessor (live, this device)"}
+
+
+def traffic_key(n_total, H, dt, month, int_mode, world, workload="rbo", steps=None, warmup=None, rl_price=None,
+                fh=0):
+    """The identity of a profiled command: workload, community, horizon and the timed window."""
+    w = f"{n_total} homes, H={H}, dt={dt}, month {month}, int_mode={int_mode}, {world} rank(s)"
+    if workload == "rl":
+        w += f", rl ({rl_price} price, forecast_horizon {fh})"
+    return w + f", timed steps {warmup}..{(warmup or 0) + (steps or 0) - 1}"
+
+
+def window(warmup, steps, dt, month, rl):
+    """The simulated time the timed steps cover (the per-step cost varies over a day)."""
+    def clock(k):
+        m = k * 60 // dt
+        return f"day {m // 1440 + 1} {m // 60 % 24:02d}:{m % 60:02d}"
+    return {"steps": [warmup, warmup + steps], "sim_hours": [warmup / dt, (warmup + steps) / dt],
+            "clock": f"{clock(warmup)} to {clock(warmup + steps)} (month {month}; step k starts at k x {60 // dt} min)",
+            "note": "timed steps k in [warmup, warmup + steps); the step cost varies with the time of day (tariff "
+                    "boundaries, daylight), so a window is not the full-day average" +
+                    ("; rl: every step is one action = rollout solves + the committed step" if rl else "")}
+
+
+from dragg_amd.community import reference_completable  # noqa: E402  (re-exported for the tools)
+
+
+def bench_community(args):
+    """The bench's synthetic community and weather (seeded; the same for every rank and tool)."""
+    from dragg_amd.community import synthetic_homes, synthetic_weather
+    dt, Hh = args.dt, args.horizon_hours
+    sim_hours = math.ceil((args.warmup + args.steps) / dt)
+    days = math.ceil((sim_hours + Hh + 2) / 24) + 1
+    homes = synthetic_homes(args.homes, seed=12, days=days, dt=dt, horizon_hours=Hh)
+    oat, ghi, tou = synthetic_weather(days, dt, sim_hours, seed=3, month=args.month)
+    return homes, oat, ghi, tou
 
 
 def main():
@@ -251,19 +340,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    from dragg_amd.community import synthetic_homes, synthetic_weather
     dt, Hh = args.dt, args.horizon_hours
     total_steps = args.warmup + args.steps
-    sim_hours = math.ceil(total_steps / dt)
-    days = math.ceil((sim_hours + Hh + 2) / 24) + 1
     n_total = args.homes
-    homes = synthetic_homes(n_total, seed=12, days=days, dt=dt, horizon_hours=Hh)
-    oat, ghi, tou = synthetic_weather(days, dt, sim_hours, seed=3, month=args.month)
+    homes, oat, ghi, tou = bench_community(args)
 
     cpu = None
+    env = {"oat": oat, "ghi": ghi, "tou": tou, "start_hour_index": 0, "reward_price": [0.0]}
+    if args.cpu_only:
+        out = cpu_baseline(homes, env, args.cpu_seconds, args.cpu_workers, args.cpu_home_steps, args.cpu_milp_limit)
+        out["workload"] = (f"{n_total} homes, H={Hh * dt} ({Hh} h), {60 // dt}-min steps, month {args.month}, "
+                           f"run_rbo_mpc closed loop from t = 0")
+        print(json.dumps(out))
+        return
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        env = {"oat": oat, "ghi": ghi, "tou": tou, "start_hour_index": 0, "reward_price": [0.0]}
-        cpu = cpu_baseline(homes, env, args.cpu_seconds, args.cpu_workers, args.cpu_home_steps)
+        cpu = cpu_baseline(homes, env, args.cpu_seconds, args.cpu_workers, args.cpu_home_steps, args.cpu_milp_limit)
 
     import torch
     from dragg_amd.aggregator import DeviceAggregator
@@ -276,14 +367,17 @@ def main():
     # (after the CPU leg: its worker processes fork before anything touches the GPU)
     replaced = None
     if not args.keep_crashing_homes:
-        homes, replaced = reference_completable(homes, oat, ghi, tou)
+        homes, replaced = reference_completable(homes, oat, ghi, tou, seed=12)
     if world > 1:
         if backend == "nccl":
             torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             torch.distributed.init_process_group(backend)
+    # keep_history: the per-step hash history (collected_data, aggregator.py:737-748) is written
+    # inside the timed steps, as a configs[2] run does
     agg = DeviceAggregator(homes, oat, ghi, tou, 0, total_steps, reward_price=[0.0],
-                           int_mode=args.int_mode, seed=12, rank=rank, world=world, keep_history=False)
+                           int_mode=args.int_mode, seed=12, rank=rank, world=world,
+                           keep_history=not args.no_history)
     stream = torch.cuda.current_stream()
 
     def barrier():
@@ -295,7 +389,12 @@ def main():
     rl = args.workload == "rl"
     fh = args.forecast_horizon if rl else 0
     import numpy as np
-    prices = np.random.default_rng(5).uniform(-0.02, 0.02, (total_steps, 1)) * np.ones((1, Hh * dt))
+    H_ = Hh * dt
+    off = np.random.default_rng(5).uniform(-0.02, 0.02, (total_steps, 1))
+    if args.rl_price == "smooth":       # changes at every stage (test_gpu_configs.py configs[4])
+        prices = off + (-0.03 * np.cos(np.arange(H_) / 3.0))[None, :]
+    else:
+        prices = off * np.ones((1, H_))
 
     def action(k):
         """rl: one reward-price action (random stand-in for the host agent's choice)."""
@@ -313,9 +412,9 @@ def main():
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
+        evs[k][0].record(stream)            # rl: the action's rollout solves are timed with its step
         if rl:
             action(args.warmup + k)
-        evs[k][0].record(stream)
         agg.run_iteration()
         evs[k][1].record(stream)
         if rl:
@@ -333,7 +432,8 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     # per-status counts of the timed steps over EVERY rank (one small all-reduce after timing)
     st = agg.status_hist[args.warmup:total_steps]
-    names = ["optimal", "infeasible", "infeasible_cert", "max_iter", "round_fail", "err_parse", "err_missing"]
+    from dragg_amd import _lib as L
+    names = L.STATUS_NAMES
     counts = torch.stack([(st == i).sum() for i in range(len(names))]).to(torch.float64)
     if world > 1:
         torch.distributed.all_reduce(counts)
@@ -347,12 +447,15 @@ def main():
         workload = (f"{n_total} homes x {args.steps} closed-loop {60 // dt}-min steps, H={H} "
                     f"({Hh} h), month {args.month}, run_rbo_mpc, int_mode={args.int_mode}")
         if rl:
-            workload = (f"{n_total} homes x {args.steps} RL reward-price actions, each {fh} rollout "
-                        f"timestep(s) + the committed {60 // dt}-min step, H={H} ({Hh} h), month {args.month}, "
-                        f"run_rl_agg, int_mode={args.int_mode}")
-        achieved = bytes_per_launch(agg.batch, success) / (kern_ms * 1e-3) / 1e9
-        pmc, traffic_src = measured_pmc(traffic_key(n_total, H, dt, args.month, args.int_mode, world))
-        traffic = pmc.get("bytes_per_launch")
+            workload = (f"{n_total} homes x {args.steps} RL reward-price actions ({args.rl_price} price), each "
+                        f"{fh} rollout timestep(s) + the committed {60 // dt}-min step, H={H} ({Hh} h), month "
+                        f"{args.month}, run_rl_agg, int_mode={args.int_mode}")
+        alg_bytes = bytes_per_launch(agg.batch, success) * (1 + fh)     # rl: per action (rollouts + commit)
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        key = traffic_key(n_total, H, dt, args.month, args.int_mode, world, args.workload, args.steps, args.warmup,
+                          args.rl_price if rl else None, fh)
+        pmc, traffic_src = measured_pmc(key)
+        traffic = pmc.get("bytes_per_step")
         out = {
             "metric": "home-MPC solves/sec (homes x steps)", "value": value, "unit": "solves/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -368,21 +471,30 @@ def main():
                        "homes_total": n_total, "homes_per_gpu": agg.batch.N, "global_batch": n_total,
                        "horizon": H, "mix": "40/20/20/20 base/pv/battery/pv_battery",
                        "parallelism": f"homes sharded x{world}"},
+            "window": window(args.warmup, args.steps, dt, args.month, rl),
+            "history_written": not args.no_history,
             "sim_wall_s": elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0,
                          "traffic": (traffic / (kern_ms * 1e-3) / 1e9) if traffic else None,
-                         "traffic_bytes_per_launch": traffic, "traffic_source": traffic_src,
+                         "traffic_bytes_per_step": traffic, "traffic_source": traffic_src,
+                         "profile_key": key,
+                         "profiled_kernel_ms_per_step": pmc.get("kernel_ms_per_step"),
                          "kernel": (f"mpc_direct_kernel (DM_FRONT + DM_BUCKET launches of a step)"
                                     if args.int_mode == "round" else "mpc_home_kernel"),
-                         "kernel_ms": kern_ms},
+                         "kernel_ms": kern_ms,
+                         "algorithmic_bytes_per_step": alg_bytes,
+                         "unit_note": "one step = the hot launch + the second launch of one timestep; HIP events "
+                                      "on the launch stream around run_iteration"},
             "cpu_baseline": cpu,
+            "cpu_baseline_full": committed_cpu_baseline() if (rank == 0 and world == 1) else None,
             "status_counts": stat_counts,
             # RL: the headline counts the rollout re-solves too; the committed steps alone:
             "committed_solves_per_s": n_total * args.steps / elapsed,
         }
-        out.update(extra_rooflines(pmc, kern_ms, agg.batch.lib.dragg_mpc_lds_bytes(ctypes.byref(agg.batch.dims)),
-                                   traffic_src))
+        out.update(extra_rooflines(pmc, traffic_src))
+        out["occupancy"] = occupancy(agg.batch) | (
+            {"wave_cycle_shares": out.pop("wave_cycle_shares")} if "wave_cycle_shares" in out else {})
         print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

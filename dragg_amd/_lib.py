@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # DRAGG_LIB: an alternative build of the same library (kernel experiments); default in-tree
 LIB_PATH = os.environ.get("DRAGG_LIB") or os.path.join(HERE, "libdragg_mi355x.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # enums (mirror include/dragg_mi355x.h)
 BASE, PV_ONLY, BATTERY_ONLY, PV_BATTERY = 0, 1, 2, 3
@@ -30,16 +30,18 @@ VAL_KEYS = FC_KEYS + ["temp_in_opt", "temp_wh_opt", "correct_solve", "solve_coun
 NVAL = len(VAL_KEYS)
 K = {k: i for i, k in enumerate(VAL_KEYS)}
 
-ST_OPTIMAL, ST_INFEASIBLE, ST_INFEASIBLE_CERT, ST_MAX_ITER, ST_ROUND_FAIL, ST_ERR_PARSE, ST_ERR_MISSING = range(7)
+(ST_OPTIMAL, ST_INFEASIBLE, ST_INFEASIBLE_CERT, ST_MAX_ITER, ST_ROUND_FAIL, ST_ERR_PARSE, ST_ERR_MISSING,
+ ST_SOLVER_ERROR) = range(8)
 # int_path bits (dragg_mi355x.h): 0-11 = a chain left the exact front DP (chain bits + reasons);
 # PATH_SECOND = the home was solved by the second launch (exact unless bits 0-11 are set)
 PATH_APPROX_MASK = 0xFFF
 PATH_SECOND = 1 << 12
+PATH_FAIL_T, PATH_FAIL_TW = 1 << 13, 1 << 14     # ROUND_FAIL decided by the indoor-air / tank chain
 STATUS_NAMES = ["optimal", "infeasible", "infeasible_cert", "max_iter", "round_fail", "err_parse",
-                "err_missing"]
+                "err_missing", "solver_error"]
 
-INT_ROUND, INT_RELAX, INT_ROUND_LP = 0, 1, 2
-INT_MODES = {"round": INT_ROUND, "relax": INT_RELAX, "round_lp": INT_ROUND_LP}
+INT_ROUND, INT_RELAX, INT_ROUND_LP, INT_FAIL = 0, 1, 2, 3
+INT_MODES = {"round": INT_ROUND, "relax": INT_RELAX, "round_lp": INT_ROUND_LP, "fail": INT_FAIL}
 
 PHASES = ["setup", "iter", "factor", "polish", "check", "integer", "write", "battery"]
 NPHASE = len(PHASES)
@@ -75,8 +77,13 @@ class Explicit(ctypes.Structure):
                 ("draw", c_dp), ("oat", c_dp), ("ghi", c_dp), ("price", c_dp)]
 
 
+class KernelInfo(ctypes.Structure):
+    _fields_ = [("vgprs", ctypes.c_int32 * 2), ("scratch_bytes", ctypes.c_int32 * 2), ("lds_bytes", ctypes.c_int32 * 2),
+                ("threads", ctypes.c_int32 * 2), ("blocks_per_cu", ctypes.c_int32 * 2)]
+
+
 EXPORTS = ["dragg_mpc_abi_version", "dragg_mpc_strerror", "dragg_mpc_lds_bytes", "dragg_mpc_workspace_bytes",
-           "dragg_mpc_step",
+           "dragg_mpc_kernel_info_get", "dragg_mpc_step",
            "dragg_mpc_solve_explicit", "dragg_mpc_aggregate", "dragg_mpc_season_noise"]
 
 _LIB = None
@@ -106,6 +113,7 @@ def load(path=LIB_PATH):
     lib.dragg_mpc_solve_explicit.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Problem),
                                              ctypes.POINTER(Explicit), ctypes.POINTER(Hash),
                                              ctypes.POINTER(Out), c_dp]
+    lib.dragg_mpc_kernel_info_get.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(KernelInfo)]
     lib.dragg_mpc_aggregate.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Hash), c_dp, c_dp]
     lib.dragg_mpc_season_noise.argtypes = [ctypes.POINTER(Dims), ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
                                            ctypes.c_int32, c_dp, c_dp]
@@ -113,6 +121,16 @@ def load(path=LIB_PATH):
         raise DraggError("ABI version mismatch between dragg_amd and libdragg_mi355x.so")
     _LIB = lib
     return lib
+
+
+def kernel_info(dims):
+    """The launches' registers, spills, LDS and resident workgroups per CU on the current device
+    (dragg_mpc_kernel_info_get): [hot launch, second launch] dicts."""
+    info = KernelInfo()
+    check(load().dragg_mpc_kernel_info_get(ctypes.byref(dims), ctypes.byref(info)))
+    return [{"vgprs": info.vgprs[i], "scratch_bytes_per_lane": info.scratch_bytes[i],
+             "lds_bytes": info.lds_bytes[i], "threads": info.threads[i],
+             "blocks_per_cu": info.blocks_per_cu[i]} for i in range(2)]
 
 
 def check(rc):

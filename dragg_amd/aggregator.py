@@ -16,6 +16,8 @@ Homes are sharded by stride (rank r solves global homes r, r + world, r + 2 worl
 shard carries the community's type mix); the season-noise stream is keyed by the GLOBAL home
 index, so results do not depend on the shard layout.
 """
+import zlib
+
 import numpy as np
 import torch
 
@@ -36,6 +38,9 @@ class DeviceAggregator:
                  int_mode="round", seed=0, rank=0, world=1, group=None, keep_history=True,
                  max_iter=4000, check_every=10, device=None, batch_cls=MPCBatch):
         self.rank, self.world, self.group = rank, world, group
+        self.seed = int(seed)
+        # identifies the community a checkpoint belongs to (load_state refuses another one's)
+        self.names_crc = zlib.crc32("\x00".join(str(h.get("name", i)) for i, h in enumerate(homes)).encode())
         self.index = shard_index(len(homes), rank, world)
         self.all_homes = homes
         self.homes = [homes[i] for i in self.index]
@@ -147,6 +152,8 @@ class DeviceAggregator:
     def save_state(self, path):
         t = self.timestep
         state = {"timestep": t, "rank": self.rank, "world": self.world, "n_local": int(self.batch.N),
+                 "seed": self.seed, "num_timesteps": int(self.num_timesteps), "n_all": len(self.all_homes),
+                 "names_crc": int(self.names_crc),
                  "vals": self.batch.vals.cpu(), "fc": self.batch.fc.cpu(),
                  "reward_price": self.batch.rp.cpu(),
                  "agg_hist": self.agg_hist[:t].cpu(), "status_hist": self.status_hist[:t].cpu(),
@@ -164,7 +171,14 @@ class DeviceAggregator:
         if (st["rank"], st["world"], st["n_local"]) != (self.rank, self.world, int(self.batch.N)):
             raise ValueError(f"checkpoint {path} is for rank {st['rank']} of {st['world']} with "
                              f"{st['n_local']} homes, not rank {self.rank} of {self.world} with {self.batch.N}")
+        want = {"seed": self.seed, "num_timesteps": int(self.num_timesteps), "n_all": len(self.all_homes),
+                "names_crc": int(self.names_crc)}
+        diff = {k: (st.get(k), v) for k, v in want.items() if st.get(k) != v}
+        if diff:
+            raise ValueError(f"checkpoint {path} belongs to another run (saved vs this run: {diff})")
         t = int(st["timestep"])
+        if not 0 <= t <= self.num_timesteps:
+            raise ValueError(f"checkpoint {path} holds timestep {t} of a {self.num_timesteps}-step run")
         self.batch.vals.copy_(st["vals"])
         self.batch.fc.copy_(st["fc"])
         self.batch.set_reward_price(st["reward_price"].to(self.device))
@@ -176,15 +190,41 @@ class DeviceAggregator:
         self.timestep = t
         return t
 
+    def agree(self, value, what):
+        """Every rank's `value` (an int) must be the same; raises on every rank otherwise (one
+        min and one max all-reduce), so that no rank goes on into a collective the others skip."""
+        if self.world == 1:
+            return int(value)
+        v = torch.tensor([int(value), -int(value)], dtype=torch.int64, device=self.agg_hist.device)
+        torch.distributed.all_reduce(v, op=torch.distributed.ReduceOp.MIN, group=self.group)
+        lo, hi = int(v[0]), -int(v[1])
+        if lo != hi:
+            raise RuntimeError(f"ranks disagree on {what}: from {lo} to {hi} (this rank: {int(value)})")
+        return lo
+
     def check_errors(self):
-        """Raise as the reference would if a home hit a crashing path (KeyError / ValueError)."""
+        """Raise as the reference would if a home hit a crashing path (KeyError / ValueError):
+        the first such (timestep, home) over EVERY rank, raised on every rank together (one
+        all-reduce), so a multi-rank run stops instead of leaving the other ranks in a gather."""
         st = self.status_hist[:self.timestep].cpu().numpy()
-        for code, exc in ((L.ST_ERR_MISSING, KeyError), (L.ST_ERR_PARSE, ValueError)):
+        n_all = max(1, len(self.all_homes))
+        first = np.iinfo(np.int64).max
+        for code in (L.ST_ERR_MISSING, L.ST_ERR_PARSE):
             bad = np.argwhere(st == code)
             if len(bad):
                 t, i = bad[0]
-                raise exc(f"home {self.homes[i]['name']} at timestep {t}: {L.STATUS_NAMES[code]} "
-                          "(the reference raises here, mpc_calc.py:280-289 / 537-539)")
+                first = min(first, (int(t) * n_all + int(self.index[i])) * 8 + code)
+        if self.world > 1:
+            v = torch.tensor([first], dtype=torch.int64, device=self.agg_hist.device)
+            torch.distributed.all_reduce(v, op=torch.distributed.ReduceOp.MIN, group=self.group)
+            first = int(v[0])
+        if first == np.iinfo(np.int64).max:
+            return
+        code = first % 8
+        t, g = divmod(first // 8, n_all)
+        exc = KeyError if code == L.ST_ERR_MISSING else ValueError
+        raise exc(f"home {self.all_homes[g]['name']} at timestep {t}: {L.STATUS_NAMES[code]} "
+                  "(the reference raises here, mpc_calc.py:280-289 / 537-539)")
 
     def collected_data(self):
         """This shard's `collected_data` dict (aggregator.py:589-615, 737-748): the initial

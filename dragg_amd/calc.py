@@ -16,11 +16,18 @@ from . import _lib as L
 from .inputs import max_load
 from .mpc import MPCBatch
 
-# The reference's plug point: home['hems']['solver'] names a cvxpy MILP backend, and an
-# unknown name falls back to GLPK_MI (mpc_calc.py:141-145).  Every one of them solves the same
-# MILP to optimality, so every one maps to this build's exact MILP path (int_mode "round");
-# the build's own modes may be named directly ("relax": the LP relaxation, "round_lp").
-SOLVER_MODES = {"GLPK_MI": "round", "GUROBI": "round", "ECOS": "round"}
+# The reference's plug point: home['hems']['solver'] names a cvxpy backend, and an unknown name
+# falls back to GLPK_MI (mpc_calc.py:141-145).  The duty variables are integer
+# (mpc_calc.py:171-173), so what a backend does depends on whether it takes a MILP:
+# * GLPK_MI (and GUROBI, when gurobipy is installed: it is not in the reference's
+#   requirements.txt, and without it cvxpy raises like ECOS below) solve the MILP to
+#   optimality -> this build's exact MILP path, int_mode "round";
+# * ECOS is not MIP-capable: cvxpy raises SolverError on an integer problem, the bare except of
+#   mpc_calc.py:450-454 sets solved = False and EVERY solve takes the fallback thermostat ->
+#   int_mode "fail" (status solver_error).  cvxpy is not pinned (requirements.txt) nor importable
+#   here, so this is parity unpinned; it follows cvxpy's documented MIP-capability check.
+# The build's own modes may be named directly ("relax": the LP relaxation, "round_lp", "fail").
+SOLVER_MODES = {"GLPK_MI": "round", "GUROBI": "round", "ECOS": "fail"}
 
 
 def int_mode_for(home):

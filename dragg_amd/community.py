@@ -135,3 +135,35 @@ def synthetic_homes(n, mix=(0.4, 0.2, 0.2, 0.2), seed=12, days=2, dt=4, horizon_
             h["pv"] = {"area": rng.uniform(*PV["area"]), "eff": rng.uniform(*PV["eff"])}
         homes.append(h)
     return homes
+
+
+def reference_completable(homes, oat, ghi, tou, seed, reward_price=(0.0,), start_index=0, rounds=8):
+    """A community the reference completes.  A battery home whose t = 0 solve fails leaves no
+    e_batt_opt in its hash, and the reference raises KeyError('e_batt_opt') at t = 1
+    (mpc_calc.py:280-289).  The failures come from the season draw (keyed by the home's index and
+    the run's `seed`: a "winter" draw on a hot day leaves the cooling duty at zero), not from the
+    home's parameters, so each such battery home swaps places with a home without a battery (whose
+    failed t = 0 solve the reference survives) until the t = 0 step solves every battery home.
+    Runs t = 0 on the GPU; deterministic (every rank builds the same community).
+    -> (homes, swaps)"""
+    import torch
+    from . import _lib as L
+    from .mpc import MPCBatch
+    homes, swaps = list(homes), 0
+    donors = [j for j in range(len(homes) - 1, -1, -1) if "battery" not in homes[j]["type"]]
+    for _ in range(rounds):
+        b = MPCBatch(homes, oat, ghi, tou, start_index, list(reward_price), int_mode="round", seed=seed)
+        b.step(0)
+        st = b.status.cpu().numpy()
+        del b
+        torch.cuda.empty_cache()
+        bad = [i for i, h in enumerate(homes) if "battery" in h["type"] and st[i] != L.ST_OPTIMAL]
+        if not bad or not donors:
+            break
+        for i in bad:
+            if not donors:
+                break
+            j = donors.pop(0)
+            homes[i], homes[j] = homes[j], homes[i]
+            swaps += 1
+    return homes, swaps

@@ -2868,6 +2868,9 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
         twhi0 = fmin(h.Twmax, h.Twmax - Kc);
     }
     int status = presolve_direct(h, D, twlo0, twhi0, lane) ? DRAGG_ST_INFEASIBLE : DRAGG_ST_OPTIMAL;
+    // a named solver that raises on the MILP (int_mode fail): the reference's except branch sets
+    // solved = False before any status exists, and cleanup_and_finish runs the fallback
+    if (a.d.int_mode == DRAGG_INT_FAIL) status = DRAGG_ST_SOLVER_ERROR;
     double* const saved = D.sc + 20;                    // step inputs, for reload_home
     if (lane == 0) {
         saved[0] = h.t; saved[1] = h.counter; saved[2] = h.winter ? 1.0 : 0.0;
@@ -2923,7 +2926,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
             const int sx = c0 ? S_T : S_TW, sv = c0 ? S_U : S_W;
             // the exact front DP; the bucketed DP only where it does not apply (mixed-sign
             // prices, a feasible set narrower than one duty step, front overflow, S != 6)
-            int r = -1;
+            int r = -5;                                    // reason 5: the exact DP not run (S != 6)
             double2* const wg = reinterpret_cast<double2*>(ws + w_region_offset(N, H)) + (size_t)home * (H + 1) * WAVE;
             if (h.S == 6 && !(MODE == DM_BUCKET && rl_prices)) {
                 double* const wl = D.wl;
@@ -2980,6 +2983,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 }
                 if (r2 < 0) int_path |= (1 << chain) | ((-r2) << (4 + 4 * chain));   // chain bit + reason
             }
+            if (!ok) int_path |= 1 << (13 + chain);        // ROUND_FAIL decided by this chain
         }
         pf.mark(DRAGG_PH_INTEGER);
         reload_home(h, a, home, saved);
@@ -3074,7 +3078,7 @@ __global__ void noise_kernel(int N, int H, uint64_t seed, int off, int stride, i
     if (2 * pr + 1 < H) out[(size_t)(2 * pr + 1) * N + home] = z1;
 }
 
-bool direct_mode(const dragg_mpc_dims* d) { return d->int_mode == DRAGG_INT_ROUND; }
+bool direct_mode(const dragg_mpc_dims* d) { return d->int_mode == DRAGG_INT_ROUND || d->int_mode == DRAGG_INT_FAIL; }
 
 size_t workspace_bytes(const dragg_mpc_dims* d) {
     // direct: [N][H][NB_CAP] u16 back-pointers, [N][8H] f64 solutions, the [N + 1] i32 list of
@@ -3091,7 +3095,7 @@ size_t kernel_lds_bytes(const dragg_mpc_dims* d) {
 
 int check_dims(const dragg_mpc_dims* d) {
     if (!d || d->n_homes < 0 || d->horizon < 1 || d->sub_steps < 1 || d->dt < 1) return DRAGG_E_ARG;
-    if (d->int_mode < DRAGG_INT_ROUND || d->int_mode > DRAGG_INT_ROUND_LP) return DRAGG_E_ARG;
+    if (d->int_mode < DRAGG_INT_ROUND || d->int_mode > DRAGG_INT_FAIL) return DRAGG_E_ARG;
     if (direct_mode(d) && d->sub_steps > 15) return DRAGG_E_ARG;     // 4-bit duty in the DP record
     if (direct_mode(d) && !direct_fits(d->horizon)) return DRAGG_E_HORIZON;
     if (kernel_lds_bytes(d) > 160 * 1024) return DRAGG_E_HORIZON;
@@ -3112,9 +3116,15 @@ int launch_kernel(K kern, int& attr_state, const KArgs& a, int blocks, int nt, s
     return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
 }
 
+// hipFuncSetAttribute is per device: the attribute state is kept per device (a process driving
+// several GPUs sets it once on each)
+constexpr int MAX_DEV = 64;
 template <bool EXPLICIT>
 int launch(const KArgs& a, hipStream_t s) {
-    static int attr[4] = {0, 0, 0, 0};
+    static int attr_dev[MAX_DEV][4] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return DRAGG_E_HIP;
+    int* const attr = attr_dev[dev];
     const int N = a.d.n_homes;
     if (!direct_mode(&a.d)) return launch_kernel(mpc_home_kernel<EXPLICIT>, attr[0], a, N, 64, kernel_lds_bytes(&a.d), s);
     if (N == 0) return DRAGG_OK;
@@ -3190,6 +3200,32 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
     KArgs a{};
     a.d = *dims; a.p = *prob; a.ex = *in; a.vals = hash->vals; a.fc = hash->fc; a.out = *out;
     return launch<true>(a, (hipStream_t)stream);
+}
+
+int dragg_mpc_kernel_info_get(const dragg_mpc_dims* dims, dragg_mpc_kernel_info* info) {
+    const int rc = check_dims(dims);
+    if (rc) return rc;
+    if (!info) return DRAGG_E_ARG;
+    *info = dragg_mpc_kernel_info{};
+    auto one = [&](const void* kern, int i, size_t lds) -> int {
+        hipFuncAttributes fa{};
+        if (hipFuncGetAttributes(&fa, kern) != hipSuccess) return DRAGG_E_HIP;
+        // the launches raise the dynamic LDS limit first (launch_kernel); so does the query
+        if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+            return DRAGG_E_LDS;
+        int blocks = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kern, WAVE, lds) != hipSuccess) return DRAGG_E_HIP;
+        info->vgprs[i] = fa.numRegs;
+        info->scratch_bytes[i] = (int32_t)fa.localSizeBytes;
+        info->lds_bytes[i] = (int32_t)lds;
+        info->threads[i] = WAVE;
+        info->blocks_per_cu[i] = blocks;
+        return DRAGG_OK;
+    };
+    if (!direct_mode(dims)) return one((const void*)mpc_home_kernel<false>, 0, kernel_lds_bytes(dims));
+    int r = one((const void*)mpc_direct_kernel<false, DM_FRONT>, 0, kernel_lds_bytes(dims));
+    if (r) return r;
+    return one((const void*)mpc_direct_kernel<false, DM_BUCKET>, 1, (size_t)big_layout(dims->horizon, dims->sub_steps).bytes);
 }
 
 int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, double* out3, void* stream) {

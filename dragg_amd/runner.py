@@ -112,16 +112,21 @@ class Aggregator:
         return os.path.join(d, f"state-rank{self.rank}-of-{self.world}.pt")
 
     # aggregator.py:757-778
-    def run_baseline(self, noise_fn=None, resume=False):
+    def run_baseline(self, noise_fn=None, resume=False, stop_after=None):
         """`noise_fn(t)`, optional: the season draw [H][homes checked] of step t (replaces the
         keyed on-device stream, e.g. to replay a recorded run).  Every checkpoint also saves
         each rank's device state; `resume=True` continues from it (the reference has no resume:
-        aggregator.py:265-267, 768) and finishes with the results an uninterrupted run writes."""
+        aggregator.py:265-267, 768) and finishes with the results an uninterrupted run writes.
+        Every rank must resume from the same timestep (a crash between two ranks' saves leaves
+        them apart): they check that together and all raise otherwise.  `stop_after`: return
+        after the first checkpoint at or past that many steps (an interrupted run)."""
         self.start_time = datetime.now()
         self._device_community()
         t0 = 0
         if resume and os.path.isfile(self.state_path()):
             t0 = self.dev.load_state(self.state_path())
+        if resume:
+            t0 = self.dev.agree(t0, "the checkpoint timestep to resume from")
             self.timestep = t0
         for t in range(t0, self.num_timesteps):
             noise = noise_fn(t)[:, self.dev.index] if noise_fn is not None else None
@@ -135,8 +140,8 @@ class Aggregator:
                 self.dev.check_errors()
                 self.write_outputs()
                 self.dev.save_state(self.state_path())
-                if getattr(self, "stop_after", None) is not None and t + 1 >= self.stop_after:
-                    return                         # (tests: a run interrupted after a checkpoint)
+                if stop_after is not None and t + 1 >= stop_after:
+                    return                         # an interrupted run
         self.dev.reduce_history()
         self.dev.check_errors()
 
@@ -319,7 +324,7 @@ class Aggregator:
         return R.write_results(self.run_dir, self.case, collected)
 
     # aggregator.py:941-970
-    def run(self, noise_fn=None, resume=False):
+    def run(self, noise_fn=None, resume=False, stop_after=None):
         sim = self.config["simulation"]
         self.checkpoint_interval = R.checkpoint_interval(sim["checkpoint_interval"], self.dt)
         self.version = sim["named_version"]
@@ -331,9 +336,15 @@ class Aggregator:
             self.case = "baseline"
             self.flush()
             self.get_homes()
-            self.run_baseline(noise_fn, resume=resume)
+            self.run_baseline(noise_fn, resume=resume, stop_after=stop_after)
+            if stop_after is not None and self.timestep < self.num_timesteps:
+                return None
             return self.write_outputs()
         if sim.get("run_rl_agg"):
+            if resume or stop_after is not None:
+                # the RL loop's state (the agent, the setpoint history, all_rps / all_sps) is not
+                # checkpointed: a resumed RL run would silently start over
+                raise ValueError("resume / stop_after are supported on the run_rbo_mpc case only")
             from .rl import agent_policy
             return self.run_rl_agg(agent_policy(self), noise_fn)
         return None

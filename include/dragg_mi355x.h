@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DRAGG_MPC_ABI_VERSION 5
+#define DRAGG_MPC_ABI_VERSION 6
 
 /* home types (aggregator.py:425, 468, 520, 555); bit 0 = pv, bit 1 = battery */
 enum dragg_home_type {
@@ -96,7 +96,9 @@ enum dragg_status {
     DRAGG_ST_MAX_ITER = 3,         /* no verified vertex within max_iter                         */
     DRAGG_ST_ROUND_FAIL = 4,       /* boxes pass presolve, but no integer duty schedule exists  */
     DRAGG_ST_ERR_PARSE = 5,        /* fallback's float(str[0]) would raise (mpc_calc.py:537)     */
-    DRAGG_ST_ERR_MISSING = 6       /* hash field missing at t>0 (KeyError, mpc_calc.py:280-289)  */
+    DRAGG_ST_ERR_MISSING = 6,      /* hash field missing at t>0 (KeyError, mpc_calc.py:280-289)  */
+    DRAGG_ST_SOLVER_ERROR = 7      /* the named solver raised: prob.solve's exception is          */
+                                   /* swallowed and the fallback runs (mpc_calc.py:450-454)       */
 };
 
 enum dragg_mpc_error {
@@ -107,7 +109,11 @@ enum dragg_mpc_error {
 enum dragg_int_mode {
     DRAGG_INT_ROUND = 0,    /* MILP, exact: thermal front DP + battery LP DP (default) */
     DRAGG_INT_RELAX = 1,    /* LP relaxation (ADMM + exact vertex polish)             */
-    DRAGG_INT_ROUND_LP = 2  /* LP relaxation for status/battery, then the integer DP  */
+    DRAGG_INT_ROUND_LP = 2, /* LP relaxation for status/battery, then the integer DP  */
+    DRAGG_INT_FAIL = 3      /* a solver that cannot take the MILP (hems.solver "ECOS": cvxpy's
+                               ECOS is not MIP-capable, so prob.solve raises inside the try of
+                               mpc_calc.py:450-454): every solve takes the fallback,
+                               status DRAGG_ST_SOLVER_ERROR                           */
 };
 
 typedef struct dragg_mpc_dims {
@@ -161,9 +167,13 @@ typedef struct dragg_mpc_out {
                                    = the indoor-air / tank chain used the bucketed
                                    approximation; bits 4-7 / 8-11 its reason: 1 mixed-sign
                                    prices, 2 a feasible set narrower than one duty step,
-                                   3 front overflow; bit 12 = solved by the second launch
+                                   3 front overflow, 4 the exact pass's bound contradicts
+                                   the bucketed schedule, 5 the exact DP was not run
+                                   (S != 6); bit 12 = solved by the second launch
                                    (its front outgrew the hot launch's capacity; still
-                                   exact when bits 0-11 are 0)                           */
+                                   exact when bits 0-11 are 0); bits 13 / 14 = status
+                                   ROUND_FAIL decided by the indoor-air / tank chain
+                                   (no integer duty schedule for it)                     */
 } dragg_mpc_out;
 
 /* solver phases timed into dragg_mpc_out.cycles (diagnostic; NULL = not stamped) */
@@ -193,6 +203,18 @@ typedef struct dragg_mpc_explicit {
     const double* price;        /* [H][N]   total_price                                 */
 } dragg_mpc_explicit;
 
+/* Resources of the solver's launches as the code object and the runtime report them
+   (hipFuncGetAttributes, hipOccupancyMaxActiveBlocksPerMultiprocessor on the current device):
+   index 0 = the hot launch (int_mode round: DM_FRONT; relax / round_lp: the LP kernel),
+   index 1 = the second launch (int_mode round; zeros otherwise). */
+typedef struct dragg_mpc_kernel_info {
+    int32_t vgprs[2];          /* registers per lane (hipFuncAttributes.numRegs)          */
+    int32_t scratch_bytes[2];  /* private memory per lane (spills; localSizeBytes)        */
+    int32_t lds_bytes[2];      /* dynamic LDS per workgroup at these dims                 */
+    int32_t threads[2];        /* threads per workgroup (one home per workgroup)          */
+    int32_t blocks_per_cu[2];  /* resident workgroups per CU at that LDS                  */
+} dragg_mpc_kernel_info;
+
 int dragg_mpc_abi_version(void);
 const char* dragg_mpc_strerror(int code);
 
@@ -216,6 +238,9 @@ int dragg_mpc_step(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob,
 int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob,
                              const dragg_mpc_explicit* in, dragg_mpc_hash* hash,
                              dragg_mpc_out* out, void* stream);
+
+/* Fill `info` for these dims (needs a GPU: queries the current device). */
+int dragg_mpc_kernel_info_get(const dragg_mpc_dims* dims, dragg_mpc_kernel_info* info);
 
 /* collect_data sums (aggregator.py:751-753): out3 = {sum p_grid_opt, sum
    forecast_p_grid_opt, sum cost_opt} over the shard's homes; an absent field (NaN: a home

@@ -41,6 +41,10 @@ SCENARIOS = {
     # BASELINE config 1: 20-home mixed community, 24 h at 15-min steps, 6 h horizon.
     "c1_h24": dict(n=20, batt=4, pv=4, pvb=4, start="2015-01-01 00", end="2015-01-02 00",
                    dt=4, horizon=6, action_horizon=6, seed=12, record_t=range(0, 96)),
+    # the same run with every MILP proven optimal (GOLDEN_MIP_REL_GAP=0, long GOLDEN_MILP_TIME_LIMIT);
+    # a record whose milp_status is still 1 (time limit, incumbent kept) is unpinned
+    "c1_h24_proven": dict(n=20, batt=4, pv=4, pvb=4, start="2015-01-01 00", end="2015-01-02 00",
+                          dt=4, horizon=6, action_horizon=6, seed=12, record_t=range(0, 96)),
     # 12 h horizon (H=48): season noise sigma reaches 1.1^47 -> mostly 'summer' -> fallback.
     "c3_h48": dict(n=6, batt=0, pv=2, pvb=0, start="2015-01-01 00", end="2015-01-01 04",
                    dt=4, horizon=12, action_horizon=12, seed=7, record_t=range(0, 16)),
@@ -154,6 +158,7 @@ def run(name, sc, hook=None):
                 milp_obj=lr["obj"] if lr else None,
                 milp_status=lr["milp_status"] if lr else None,
                 milp_gap=_f(lr["mip_gap"]) if lr else None,
+                milp_seconds=_f(lr.get("milp_seconds")) if lr else None,
                 lp_status=int(lr["relax_status"]) if lr else None,
                 lp_obj=lr["relax_obj"] if lr else None,
                 prev_hash=prev if self.prob.status != "optimal" else {},

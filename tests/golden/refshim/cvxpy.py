@@ -282,7 +282,9 @@ class Problem:
 
     def solve(self, solver=None, verbose=False, **kw):
         vars_, order, off, cobj, A_eq, b_eq, A_ub, b_ub, integ, c0 = self._assemble()
+        t_start = __import__("time").time()
         res = self._run(cobj, A_eq, b_eq, A_ub, b_ub, integ)
+        t_milp = __import__("time").time() - t_start
         relax = self._run(cobj, A_eq, b_eq, A_ub, b_ub, np.zeros_like(integ))
         # HiGHS milp status: 0 optimal, 1 iteration/time limit, 2 infeasible, 3 unbounded, 4 other
         status = {0: "optimal", 2: "infeasible", 3: "unbounded"}.get(res.status, "solver_error")
@@ -293,7 +295,7 @@ class Problem:
         Problem.last_record = dict(cobj=cobj, A_eq=A_eq, b_eq=b_eq, A_ub=A_ub, b_ub=b_ub, integ=integ,
                                    order=[(vars_[k], off[k]) for k in order],
                                    status=status, milp_status=int(res.status),
-                                   mip_gap=getattr(res, "mip_gap", None), x=None if res.x is None else res.x.copy(),
+                                   mip_gap=getattr(res, "mip_gap", None), milp_seconds=t_milp, x=None if res.x is None else res.x.copy(),
                                    obj=None if res.x is None else float(res.fun + c0),
                                    relax_status=relax.status,
                                    relax_x=None if relax.x is None else relax.x.copy(),

@@ -9,9 +9,12 @@ to a sequential run.
 """
 import multiprocessing as mp
 import os
+import sys
+import time
 
 EXTRA = []          # golden records appended by the harness inside a worker
 WORKERS = int(os.environ.get("GOLDEN_WORKERS", "8"))
+_CALLS, _T0 = [0], time.time()
 
 
 def _work(args):
@@ -38,4 +41,7 @@ class ProcessPool:
         for journal, extra in outs:
             R.replay(journal)
             EXTRA.extend(extra)
+        _CALLS[0] += 1
+        print(f"[pool] map #{_CALLS[0]}: {len(items)} items, {time.time() - _T0:.0f}s since start",
+              file=sys.stderr, flush=True)
         return [None] * len(items)

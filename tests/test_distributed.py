@@ -200,3 +200,69 @@ def test_checkpoint_roundtrip(tmp_path):
     other = DeviceAggregator(homes, [0.0], [0.0], [0.0], rank=1, world=2, **kw)
     with pytest.raises(ValueError):
         other.load_state(path)
+
+
+# ------------------------------------------------------------------ resume / errors over 2 ranks
+class ErrBatch(StateBatch):
+    """StateBatch whose global home 3 hits the reference's KeyError path at t = 2."""
+
+    def step(self, t, noise=None, hist=None):
+        super().step(t, noise, hist)
+        from dragg_amd import _lib as L
+        self.status = torch.where((self.gidx == 3) & (t >= 2), L.ST_ERR_MISSING, 0).to(torch.int32)
+
+
+def _resume_worker(rank, world, port, root, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    homes = [{"name": f"h{i}"} for i in range(6)]
+    kw = dict(num_timesteps=6, rank=rank, world=world, device=torch.device("cpu"), batch_cls=StateBatch)
+    out = {}
+    # a crash between the two ranks' saves: rank 0 checkpointed step 3, rank 1 still holds step 2
+    a = DeviceAggregator(homes, [0.0], [0.0], [0.0], **kw)
+    for _ in range(2 + (rank == 0)):             # (no reduce_history: the ranks never met)
+        a.run_iteration()
+        a.collect_data(defer=True)
+    path = os.path.join(root, f"state-{rank}.pt")
+    a.save_state(path)
+    b = DeviceAggregator(homes, [0.0], [0.0], [0.0], **kw)
+    try:
+        b.agree(b.load_state(path), "the checkpoint timestep")
+        out["resume"] = "ok"
+    except RuntimeError as e:
+        out["resume"] = str(e)
+    # the same checkpoint under another seed is another run's
+    c = DeviceAggregator(homes, [0.0], [0.0], [0.0], seed=99, **kw)
+    try:
+        c.load_state(path)
+        out["seed"] = "ok"
+    except ValueError as e:
+        out["seed"] = "refused"
+    # a crashing home on rank 1 only: both ranks raise the same KeyError together
+    kw["batch_cls"] = ErrBatch
+    d = DeviceAggregator(homes, [0.0], [0.0], [0.0], **kw)
+    d.run_baseline(steps=4)
+    try:
+        d.check_errors()
+        out["err"] = "ok"
+    except KeyError as e:
+        out["err"] = str(e)
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_two_ranks_resume_disagreement_and_errors_raise_on_every_rank(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_resume_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for rank in (0, 1):
+        assert "ranks disagree" in res[rank]["resume"] and "from 2 to 3" in res[rank]["resume"]
+        assert res[rank]["seed"] == "refused"
+        assert "home h3 at timestep 2" in res[rank]["err"]

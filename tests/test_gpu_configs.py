@@ -14,9 +14,11 @@ test runs the whole workload on the device and then checks a sample of its solve
   c.x = objective).
 
 Synthetic communities can contain battery homes whose t = 0 solve fails; the reference then
-raises KeyError('e_batt_opt') at t = 1 (mpc_calc.py:280-289).  Such a run is not one the
-reference completes: the tests assert that check_errors() raises exactly that, and that every
-such home is a battery home whose t = 0 solve failed.
+raises KeyError('e_batt_opt') at t = 1 (mpc_calc.py:280-289), and a run that stops at t = 1 is
+not a run of the reference.  The at-size tests therefore run communities the reference completes
+(dragg_amd.community.reference_completable, the bench's rule: such battery homes swap places
+with homes without a battery) and require no error; test_crashing_community_raises_the_references
+_keyerror keeps one small community as drawn and asserts the reference's KeyError path.
 """
 import math
 
@@ -26,12 +28,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _community(n, hours, dt, steps, month, seed):
-    from dragg_amd.community import synthetic_homes, synthetic_weather
+def _community(n, hours, dt, steps, month, seed, completable=True, rp=(0.0,)):
+    from dragg_amd.community import synthetic_homes, synthetic_weather, reference_completable
     sim_hours = math.ceil(steps / dt)
     days = math.ceil((sim_hours + hours + 2) / 24) + 1
     homes = synthetic_homes(n, seed=seed, days=days, dt=dt, horizon_hours=hours)
     oat, ghi, tou = synthetic_weather(days, dt, sim_hours, seed=seed + 1, month=month)
+    if completable:
+        homes, _ = reference_completable(homes, oat, ghi, tou, seed=seed, reward_price=rp)
     return homes, oat, ghi, tou
 
 
@@ -128,10 +132,10 @@ def _sample(rng, status, homes, per_type):
     return np.array(out)
 
 
-def _run(n, hours, dt, steps, month, seed, sample_steps, per_type, rp=(0.0,), keep_history=True):
+def _run(n, hours, dt, steps, month, seed, sample_steps, per_type, rp=(0.0,), keep_history=True, completable=True):
     import torch
     from dragg_amd.aggregator import DeviceAggregator
-    homes, oat, ghi, tou = _community(n, hours, dt, steps, month, seed)
+    homes, oat, ghi, tou = _community(n, hours, dt, steps, month, seed, completable, rp)
     agg = DeviceAggregator(homes, oat, ghi, tou, 0, steps, reward_price=list(rp), seed=seed,
                            keep_history=keep_history)
     rng = np.random.default_rng(seed)
@@ -153,11 +157,13 @@ def _run(n, hours, dt, steps, month, seed, sample_steps, per_type, rp=(0.0,), ke
     return homes, agg, checked
 
 
-def _report(tag, agg, homes, checked, min_opt=50):
+def _report(tag, agg, homes, checked, min_opt=50, completable=True):
     from dragg_amd import _lib as L
     st = agg.status_hist[:agg.timestep].cpu().numpy()
     counts = {L.STATUS_NAMES[c]: int((st == c).sum()) for c in np.unique(st)}
     n_err = _errors_are_the_references(agg, homes)
+    if completable:                                  # a run the reference completes: no crash path
+        assert n_err == 0 and not (st == L.ST_ERR_MISSING).any()
     n_opt = sum(c[1] for c in checked)
     n_none = sum(c[2] for c in checked)
     print(f"{tag}: {st.size} solves {counts}; homes on the reference's KeyError path: {n_err}; "
@@ -182,6 +188,16 @@ def test_config1_1k_homes_h24_96_steps(gpu):
     assert np.allclose(got[ok], want[ok], rtol=1e-12, atol=1e-9)
 
 
+def test_crashing_community_raises_the_references_keyerror(gpu):
+    """configs[1]'s community as drawn (no swaps) holds battery homes whose t = 0 solve fails:
+    the reference raises KeyError('e_batt_opt') at t = 1 (mpc_calc.py:280-289); check_errors()
+    raises exactly that, for battery homes whose t = 0 solve failed, and nothing else differs."""
+    homes, agg, checked = _run(1000, 6, 4, 4, 1, 31, sample_steps={0, 1}, per_type=25, completable=False)
+    st = _report("configs[1] community as drawn, 4 steps", agg, homes, checked, min_opt=20, completable=False)
+    from dragg_amd import _lib as L
+    assert (st == L.ST_ERR_MISSING).any()
+
+
 def test_config3_100k_homes_7_days(gpu):
     """configs[3]: 100,000 homes, 7 days at 15-min steps (672 steps), device-resident state,
     no per-step history (keep_history=False)."""
@@ -201,7 +217,7 @@ def test_config4_rl_10k_homes_price_broadcast_and_rollouts(gpu):
     import torch
     from dragg_amd import _lib as L
     from dragg_amd.aggregator import DeviceAggregator
-    homes, oat, ghi, tou = _community(10000, 12, 4, 8, 7, 51)
+    homes, oat, ghi, tou = _community(10000, 12, 4, 8, 7, 51, rp=[0.0] * 48)
     agg = DeviceAggregator(homes, oat, ghi, tou, 0, 8, reward_price=[0.0] * 48, seed=51)
     for _ in range(2):
         agg.run_iteration()

@@ -167,3 +167,44 @@ def test_per_home_facade_matches_batch(gpu):
         for i, c in enumerate(calcs):
             assert com.hgetall(c.name) == ref.batch.hash_dict(i)
             assert c.optimal_vals["temp_in_opt"] == float(ref.batch.hash_dict(i)["temp_in_opt"])
+
+
+def test_ecos_solver_every_solve_falls_back(gpu):
+    """hems.solver = "ECOS" (mpc_calc.py:141): cvxpy's ECOS is not MIP-capable, prob.solve raises
+    inside the try of mpc_calc.py:450-454 and cleanup_and_finish runs the fallback at every step.
+    The device run (int_mode "fail") is compared with the oracle's run_home_step under a solver
+    that raises, hash for hash as redis strings; battery homes hit the reference's KeyError at
+    t = 1 (no e_batt_opt was ever written, mpc_calc.py:280-289).  Parity unpinned on the cvxpy
+    side (cvxpy is absent: its MIP-capability check is restated, not run)."""
+    import torch
+    from dragg_amd import _lib as L
+    from dragg_amd.calc import int_mode_for
+    from oracle import mpc as M
+    d = F.load("c1_h24")
+    env = d["env"]
+    homes = [dict(h, hems=dict(h["hems"], solver="ECOS")) for h in d["homes"]]
+    assert int_mode_for(homes[0]) == "fail"
+    from dragg_amd.mpc import MPCBatch
+    b = MPCBatch(homes, env["oat"], env["ghi"], env["tou_window"], 0, [0.0] * 24, int_mode="fail")
+    hcs = [M.home_const(h) for h in homes]
+    hashes = [{} for _ in homes]
+    oenv = {"oat": env["oat"], "ghi": env["ghi"], "tou": env["tou_window"], "start_hour_index": 0,
+            "reward_price": [0.0] * 24}
+
+    def raises(P):
+        raise RuntimeError("Problem is mixed-integer, but candidate QP/Conic solvers ([ECOS]) are not MIP-capable")
+    rng = np.random.default_rng(8)
+    for t in range(4):
+        noise = rng.standard_normal((b.H, b.N))
+        b.step(t, noise=torch.tensor(noise))
+        torch.cuda.synchronize()
+        st = b.status.cpu().numpy()
+        for i, h in enumerate(homes):
+            if "battery" in h["type"] and t >= 1:
+                assert st[i] == L.ST_ERR_MISSING, (h["name"], t)
+                with pytest.raises(KeyError):
+                    M.run_home_step(hcs[i], t, dict(hashes[i]), oenv, noise[:, i], solver=raises)
+                continue
+            status, _, _ = M.run_home_step(hcs[i], t, hashes[i], oenv, noise[:, i], solver=raises)
+            assert status is None and st[i] == L.ST_SOLVER_ERROR, (h["name"], t, st[i])
+            assert b.hash_dict(i) == hashes[i], (h["name"], t)

@@ -176,12 +176,13 @@ def test_size_queries_without_gpu(lib_path):
 
 
 def test_solver_name_plug_point():
-    """home['hems']['solver'] (mpc_calc.py:141-145): every MILP backend name -- and an unknown
-    name, which the reference replaces by GLPK_MI -- selects the exact MILP path; the build's
-    own int_mode names select themselves."""
+    """home['hems']['solver'] (mpc_calc.py:141-145): the MILP backends -- and an unknown name,
+    which the reference replaces by GLPK_MI -- select the exact MILP path; ECOS, which cvxpy
+    refuses on an integer problem (every solve falls back, mpc_calc.py:450-454), selects the
+    always-fallback mode; the build's own int_mode names select themselves."""
     from dragg_amd.calc import int_mode_for
-    for name, mode in (("GLPK_MI", "round"), ("GUROBI", "round"), ("ECOS", "round"), ("nonsense", "round"),
-                       ("relax", "relax"), ("round_lp", "round_lp")):
+    for name, mode in (("GLPK_MI", "round"), ("GUROBI", "round"), ("ECOS", "fail"), ("nonsense", "round"),
+                       ("relax", "relax"), ("round_lp", "round_lp"), ("fail", "fail")):
         assert int_mode_for({"hems": {"solver": name}}) == mode
     assert int_mode_for({"hems": {}}) == "round"
 

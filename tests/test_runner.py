@@ -133,8 +133,7 @@ def test_runner_resume_from_checkpoint(gpu, tmp_path):
         f.write(txt)
     full = Aggregator(data_dir=str(data), outputs_dir=str(tmp_path / "full")).run()
     a = Aggregator(data_dir=str(data), outputs_dir=str(tmp_path / "split"))
-    a.stop_after = 8                                  # "crash" after the second hourly checkpoint
-    a.run()
+    assert a.run(stop_after=8) is None                # "crash" after the second hourly checkpoint
     assert os.path.isfile(a.state_path())
     b = Aggregator(data_dir=str(data), outputs_dir=str(tmp_path / "split"))
     path = b.run(resume=True)

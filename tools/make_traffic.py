@@ -1,10 +1,18 @@
 #!/usr/bin/env python3
-"""profiles/<round>/traffic.json from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
-tools/gpu_profile.sh: HBM bytes per launch of the solver kernel = (2 x FETCH_SIZE +
-WRITE_SIZE) x 1024 (MI355X_MICROARCH.md §HBM: FETCH_SIZE counts half of a streaming read on
-gfx950; our reads are narrow, so the factor is an upper estimate).  Also the SQ counters of
-the sq1 / sq2 passes per launch (VALU/LDS/SALU instruction counts, wave cycles in quad-cycles),
-from which bench.py prices the kernel against the VALU issue rate."""
+"""profiles/<round>/traffic*.json from the rocprofv3 passes of ONE bench command (tools/gpu_profile.sh):
+the kernel trace and the PMC passes (each counter group in its own run of the same command).
+
+Only the TIMED steps count: the last `--steps` step groups of every pass (a step group = the hot
+launch `mpc_direct_kernel<false, 0>` and the launches after it up to the next one, i.e. the
+second launch of the same timestep; for the RL workload one action = forecast_horizon rollout
+steps + the committed step).  Per step (per action for RL):
+* kernel_ms_per_step: summed durations of the step group's launches (kernel trace);
+* bytes_per_step: HBM bytes (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (MI355X_MICROARCH.md HBM section:
+  FETCH_SIZE counts half of a streaming read on gfx950; our reads are narrow, so the factor is an
+  upper estimate);
+* sq_per_step: the SQ counters of the sq* passes;
+* front_stats (optional, tools/front_stats.py on the same window): label relaxations per step.
+bench.py uses the file only when its key names the same workload and timed window."""
 import argparse
 import csv
 import json
@@ -15,18 +23,51 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def per_dispatch(path, counter, kernel_sub):
-    """Per solver STEP: the step's launches (DM_FRONT and the DM_BUCKET second launch, both named
-    mpc_direct_kernel) summed, averaged over the steps (= the DM_FRONT dispatches) -- the unit
-    bench.py times with its events around run_iteration."""
-    vals, first = {}, set()
+def _hot(name):
+    return "mpc_direct_kernel<false, 0>" in name or "mpc_home_kernel<false>" in name
+
+
+def step_groups(rows, n_units, per_unit, kernel_sub="mpc_"):
+    """rows: (dispatch_id, kernel_name, payload) of one pass.  -> the last n_units units, each a list
+    of payloads (a unit = per_unit consecutive step groups)."""
+    rows = sorted((r for r in rows if kernel_sub in r[1]), key=lambda r: r[0])
+    groups = []
+    for d, name, pay in rows:
+        if _hot(name) or not groups:
+            groups.append([])
+        groups[-1].append(pay)
+    need = n_units * per_unit
+    if len(groups) < need:
+        raise SystemExit(f"only {len(groups)} step groups in the pass, {need} needed")
+    groups = groups[-need:]
+    return [sum(groups[u * per_unit:(u + 1) * per_unit], []) for u in range(n_units)]
+
+
+def trace_ms(path, n_units, per_unit):
+    rows = []
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter and kernel_sub in r["Kernel_Name"]:
-            vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-            if "<false, 0>" in r["Kernel_Name"] or "<true, 0>" in r["Kernel_Name"] or "direct" not in kernel_sub:
-                first.add(r["Dispatch_Id"])
-    steps = max(1, len(first) or len(vals))
-    return sum(vals.values()) / steps, steps
+        rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"],
+                     (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6))
+    units = step_groups(rows, n_units, per_unit)
+    per = [sum(u) for u in units]
+    return sum(per) / len(per), per
+
+
+def counters(path, n_units, per_unit):
+    """{counter: mean per unit} over the last n_units units of a PMC pass."""
+    by = {}
+    for r in csv.DictReader(open(path)):
+        by.setdefault(r["Counter_Name"], []).append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
+    out = {}
+    for c, rows in by.items():
+        # a dispatch may report several rows of one counter (per XCD/instance): sum them first
+        agg = {}
+        for d, name, v in rows:
+            agg.setdefault((d, name), 0.0)
+            agg[(d, name)] += v
+        units = step_groups([(d, n, v) for (d, n), v in agg.items()], n_units, per_unit)
+        out[c] = sum(sum(u) for u in units) / len(units)
+    return out
 
 
 def main():
@@ -39,32 +80,42 @@ def main():
     ap.add_argument("--month", type=int, default=7)
     ap.add_argument("--int-mode", default="round")
     ap.add_argument("--world", type=int, default=1)
-    ap.add_argument("--kernel", default="mpc_direct_kernel")
+    ap.add_argument("--workload", default="rbo")
+    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--warmup", type=int, required=True)
+    ap.add_argument("--rl-price", default="smooth")
+    ap.add_argument("--forecast-horizon", type=int, default=1)
+    ap.add_argument("--command", default="")
     a = ap.parse_args()
     from bench import traffic_key
-    fetch, nf = per_dispatch(os.path.join(a.prof, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE", a.kernel)
-    write, nw = per_dispatch(os.path.join(a.prof, "write", "write_counter_collection.csv"), "WRITE_SIZE", a.kernel)
-    out = {"workload": traffic_key(a.homes, a.horizon, a.dt, a.month, a.int_mode, a.world),
-           "kernel": a.kernel, "dispatches": [nf, nw],
-           "fetch_size_kb_per_launch": fetch, "write_size_kb_per_launch": write,
-           "bytes_per_launch": (2.0 * fetch + write) * 1024.0,
-           "formula": "(2 x FETCH_SIZE + WRITE_SIZE) x 1024, rocprofv3 --pmc, separate passes"}
+    rl = a.workload == "rl"
+    fh = a.forecast_horizon if rl else 0
+    per_unit = 1 + fh
+    key = traffic_key(a.homes, a.horizon, a.dt, a.month, a.int_mode, a.world, a.workload, a.steps, a.warmup,
+                      a.rl_price if rl else None, fh)
+    ms, per = trace_ms(os.path.join(a.prof, "trace", "trace_kernel_trace.csv"), a.steps, per_unit)
+    out = {"workload": key, "command": a.command, "unit": "action" if rl else "step",
+           "kernel_ms_per_step": ms, "kernel_ms_per_step_min_max": [min(per), max(per)]}
+    f = counters(os.path.join(a.prof, "fetch", "fetch_counter_collection.csv"), a.steps, per_unit)["FETCH_SIZE"]
+    w = counters(os.path.join(a.prof, "write", "write_counter_collection.csv"), a.steps, per_unit)["WRITE_SIZE"]
+    out.update({"fetch_size_kb_per_step": f, "write_size_kb_per_step": w, "bytes_per_step": (2.0 * f + w) * 1024.0,
+                "formula": "(2 x FETCH_SIZE + WRITE_SIZE) x 1024, rocprofv3 --pmc, separate passes"})
     sq = {}
     for p in ("sq1", "sq2", "sq3", "sq4"):
-        f = os.path.join(a.prof, p, f"{p}_counter_collection.csv")
-        if not os.path.exists(f):
-            continue
-        for c in sorted({r["Counter_Name"] for r in csv.DictReader(open(f))}):
-            sq[c] = per_dispatch(f, c, a.kernel)[0]
+        fp = os.path.join(a.prof, p, f"{p}_counter_collection.csv")
+        if os.path.exists(fp):
+            sq.update(counters(fp, a.steps, per_unit))
     if sq:
-        out["sq_per_launch"] = sq
+        out["sq_per_step"] = sq
     fs = os.path.join(a.prof, "front_stats.json")
     if os.path.exists(fs):
-        with open(fs) as f:
-            out["front_stats"] = json.load(f)
-    os.makedirs(os.path.dirname(a.out), exist_ok=True)
-    with open(a.out, "w") as f:
-        json.dump(out, f, indent=1)
+        with open(fs) as fh_:
+            st = json.load(fh_)
+        if st.get("window") == [a.warmup, a.warmup + a.steps]:
+            out["front_stats"] = st
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+    with open(a.out, "w") as fh_:
+        json.dump(out, fh_, indent=1)
     print(json.dumps(out))
 
 
