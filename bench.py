@@ -61,6 +61,9 @@ def parse(argv=None):
                          "(-0.03 cos(k/3) + a per-action offset, the shape of test_gpu_configs.py's "
                          "configs[4] test: the price changes at every stage); 'flat' "
                          "is one constant per action (round 2's RL line)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="diagnostic: time rank 0's strided shard of the community sharded this many ways, on "
+                         "one GPU without the collectives (the per-GPU load of an N-GPU strong-scaling run)")
     ap.add_argument("--no-history", action="store_true",
                     help="skip the per-step history write (collected_data); a configs[2] run keeps it")
     ap.add_argument("--keep-crashing-homes", action="store_true",
@@ -375,9 +378,12 @@ def main():
             torch.distributed.init_process_group(backend)
     # keep_history: the per-step hash history (collected_data, aggregator.py:737-748) is written
     # inside the timed steps, as a configs[2] run does
+    shard = args.shard_of > 1 and world == 1
     agg = DeviceAggregator(homes, oat, ghi, tou, 0, total_steps, reward_price=[0.0],
-                           int_mode=args.int_mode, seed=12, rank=rank, world=world,
+                           int_mode=args.int_mode, seed=12, rank=rank, world=args.shard_of if shard else world,
                            keep_history=not args.no_history)
+    if shard:
+        agg.world = 1                     # one GPU: no collectives (the shard's own sums)
     stream = torch.cuda.current_stream()
 
     def barrier():
@@ -440,7 +446,7 @@ def main():
     counts = counts.cpu().tolist()
     stat_counts = {name: int(c) for name, c in zip(names, counts)}
     success = stat_counts["optimal"] / max(1, sum(stat_counts.values()))
-    solves = n_total * args.steps * (1 + fh)
+    solves = (agg.batch.N if shard else n_total) * args.steps * (1 + fh)
     value = solves / elapsed
     if rank == 0:
         H = agg.batch.H
@@ -471,6 +477,10 @@ def main():
                        "homes_total": n_total, "homes_per_gpu": agg.batch.N, "global_batch": n_total,
                        "horizon": H, "mix": "40/20/20/20 base/pv/battery/pv_battery",
                        "parallelism": f"homes sharded x{world}"},
+            "shard_emulation": ({"shard_of": args.shard_of, "homes": agg.batch.N,
+                                 "note": "diagnostic: rank 0's strided shard alone on one GPU (the per-GPU load of "
+                                         "an N-GPU strong-scaling run), no collectives; value counts the shard's "
+                                         "solves"} if shard else None),
             "window": window(args.warmup, args.steps, dt, args.month, rl),
             "history_written": not args.no_history,
             "sim_wall_s": elapsed,

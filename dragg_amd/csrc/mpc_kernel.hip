@@ -43,6 +43,9 @@ constexpr int NTB_HOT = 64;           // key / cost buckets per stage of the hot
                                       //   (small fronts: a one-bucket-per-lane scan; measured 128: +6 % time)
 constexpr int NTB = 192;              // ... of the second launch's regular front DP and round_lp
 constexpr int NTB_BIG = 256;          // ... of the big exact pass (fronts up to NF_BIG)
+// exchange area of a multi-wave front DP: per-pass survivor masks, per-wave counts / ranges / minima
+constexpr int XCH_PASSES = 32;
+constexpr int XCH_BYTES = XCH_PASSES * 8 + 8 * 8 + 8 * 5 * 4;
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
 
 constexpr double SIGMA = 1e-6;
@@ -1024,8 +1027,8 @@ DEV bool dp_chain(const Home& h, const Lds& L, const DpChain& c, int lane) {
     return true;
 }
 
-template <int SS, int CAP = NF, int CAPB = NF_BOUND, int PS = NB_CAP, int NBK = NTB>
-DEV int dp_front(const struct FrontBufs& B, int H, int lane, double g, double x0, double lo0, double hi0, double lo,
+template <int SS, int CAP = NF, int CAPB = NF_BOUND, int PS = NB_CAP, int NBK = NTB, int NW = 1>
+DEV int dp_front(const struct FrontBufs& B, int H, int tid, double g, double x0, double lo0, double hi0, double lo,
                  double hi, int sx, int sv, bool use_bound = false, double ub_ext = INFINITY,
                  double* best_out = nullptr);
 
@@ -1404,6 +1407,7 @@ struct LdsD {
     double *sgS, *sgL;                  // battery segments [2][seg_cap], in lab / rmin (the
                                         //   battery LP runs after the thermal DPs)
     double* wl;                         // [3][WAVE] dp_front's W table (points, values, slopes)
+    char* xch;                          // [XCH_BYTES] front_layout: a multi-wave DP's exchange area
     uint16_t* par;                      // [H][NB_CAP] DP back-pointers (global workspace)
 };
 
@@ -1441,7 +1445,7 @@ struct DirectLayout {
     int draw, oat, ghi, price, cA, cC, cq, sc, t2, bx0, bp1, bp2, lab, rmin, tail;
     int kb, cb, mh, kl, flo, fhi;             // dp_front tail
     int cand, rt, candp, tarr, rsrc;          // dp_zspace tail
-    int wl, sgS, sgL;                         // front_layout only: W table, battery segment lists
+    int wl, sgS, sgL, xch;                    // front_layout only: W table, battery segment lists, exchange
     int bytes;
 };
 
@@ -1471,6 +1475,7 @@ __host__ __device__ inline DirectLayout front_layout(int H) {
     o.kl = take(4 * NTB_HOT, 4);
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
+    o.xch = take(XCH_BYTES, 16);
     const int dp_end = p;
     p = o.tail;                                  // the battery LP's arrays over the dead DP region
     o.sgS = take(16 * seg_cap(H), 16);
@@ -1571,6 +1576,7 @@ DEV LdsD carve_front(double* smem, int H) {
     L.fhi = reinterpret_cast<unsigned*>(b + o.fhi);
     L.sgS = D(o.sgS); L.sgL = D(o.sgL);
     L.bx0 = D(o.bx0); L.bp1 = D(o.bp1); L.bp2 = D(o.bp2); L.t2 = D(o.t2);
+    L.xch = b + o.xch;
     L.par = nullptr;                                             // set by the kernel
     return L;
 }
@@ -2210,6 +2216,7 @@ struct FrontBufs {
     double2* wg;                         // [H + 1][WAVE] global: LP cost-to-go W_j as points (x, v),
                                          //   +inf padded; nullptr = no bound pruning
     double *wlx, *wlv, *wls;             // [WAVE] LDS: the current stage's W (points, slopes)
+    char* xch;                           // [XCH_BYTES] LDS: the waves' exchange area (NW > 1)
 };
 
 // 1 / w to about 1 ulp: v_rcp_f64 and one Newton step (no IEEE division sequence)
@@ -2263,9 +2270,20 @@ DEV T dpp_iscan(T v, int lane, T id, Op op) {
     return row == 0 ? v : op(v, off);
 }
 
-template <int SS, int CAP, int CAPB, int PS, int NBK>
-DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, double lo0, double hi0, double lo,
+template <int SS, int CAP, int CAPB, int PS, int NBK, int NW>
+DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double lo0, double hi0, double lo,
                  double hi, int sx, int sv, bool use_bound, double ub_ext, double* best_out) {
+    // NW waves share one home's DP (latency: few homes per GPU): every wave runs the same
+    // uniform control flow (W table, hulls and scans are computed redundantly or by wave 0), the
+    // children of a stage are split into contiguous pass ranges per wave, and survivors keep the
+    // single-wave (parent, duty) order: the fronts, and so the result, are bit-identical for any NW
+    constexpr int NT = NW * WAVE;
+    const int lane = tid & (WAVE - 1);
+    const int wid = NW > 1 ? tid / WAVE : 0;
+    static_assert(NW == 1 || CAP * (SS + 1) <= XCH_PASSES * WAVE, "the exchange area holds 32 passes");
+    unsigned long long* const xmask = reinterpret_cast<unsigned long long*>(B.xch);
+    double* const xbest = reinterpret_cast<double*>(B.xch + XCH_PASSES * 8);
+    unsigned* const xint = reinterpret_cast<unsigned*>(B.xch + XCH_PASSES * 8 + 8 * 8);   // [5][8]
     static_assert(SS > 0 && SS < 16, "duty count must be a compile-time constant below 16");
     static_assert(CAP <= PS && CAPB <= PS && PS <= 4096, "back-pointer rows hold a 12-bit parent index");
     constexpr int NU = SS + 1;
@@ -2302,7 +2320,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         double l = H == 1 ? lo0 : lo, u = H == 1 ? hi0 : hi;
         l -= tw(l);
         u += tw(u);
-        if (lane == 0) { B.flo[H] = enc_lo(l); B.fhi[H] = enc_hi(u); }
+        if (tid == 0) { B.flo[H] = enc_lo(l); B.fhi[H] = enc_hi(u); }
         const double gmin = fmin(0.0, g * SS), gmax = fmax(0.0, g * SS);
         for (int k = H - 1; k >= 1 && !empty; --k) {
             narrow = narrow || (u - l < fabs(g));
@@ -2315,7 +2333,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             l -= tw(l);
             u += tw(u);
             empty = l > u;
-            if (lane == 0) { B.flo[k] = enc_lo(l); B.fhi[k] = enc_hi(u); }
+            if (tid == 0) { B.flo[k] = enc_lo(l); B.fhi[k] = enc_hi(u); }
         }
         if (empty) return 0;
         nodom = nodom || narrow;
@@ -2349,7 +2367,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             bh += tw(bh);
             double wx = lane == 0 ? bl : lane == 1 ? bh : INFINITY, wv = lane < 2 ? 0.0 : INFINITY;
             int m = 2;
-            if (lane < m) B.wg[H * WAVE + lane] = make_double2(wx, wv);
+            if (wid == 0 && lane < m) B.wg[H * WAVE + lane] = make_double2(wx, wv);
             set_count(H, m);
             for (int j = H - 1; j >= 1; --j) {
                 const double A = B.cA[j], C = B.cC[j], q = B.cq[j];
@@ -2378,12 +2396,12 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
                 const int m2 = __popcll(bal) + 2;
                 if (m2 > WAVE) { prune = false; break; }
                 // compact through the LDS table (free here)
-                if (in) {
+                if (wid == 0 && in) {
                     const int pos_ = 1 + __popcll(bal & ((1ull << lane) - 1ull));
                     B.wlx[pos_] = nx;
                     B.wlv[pos_] = nv;
                 }
-                if (lane == 0) {
+                if (tid == 0) {
                     B.wlx[0] = dl; B.wlv[0] = vdl;
                     B.wlx[m2 - 1] = dh; B.wlv[m2 - 1] = vdh;
                 }
@@ -2392,7 +2410,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
                 wv = lane < m2 ? B.wlv[lane] : INFINITY;
                 m = m2;
                 __syncthreads();
-                if (lane < m) B.wg[j * WAVE + lane] = make_double2(wx, wv);
+                if (wid == 0 && lane < m) B.wg[j * WAVE + lane] = make_double2(wx, wv);
                 set_count(j, m);
             }
         }
@@ -2405,10 +2423,11 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             qabs = dpp_sum(qabs);
             double gx = x0, ub = 0.0;
             bool gok = true;
-            double2 cur = load_row(1);
+            // (the W table is wave 0's to load and write; every wave reads it)
+            double2 cur = wid == 0 ? load_row(1) : make_double2(INFINITY, INFINITY);
             for (int k = 0; k < H && gok; ++k) {
-                double2 nxt = k + 2 <= H ? load_row(k + 2) : make_double2(INFINITY, INFINITY);
-                w_to_lds(B, lane, cur.x, cur.y);
+                double2 nxt = (wid == 0 && k + 2 <= H) ? load_row(k + 2) : make_double2(INFINITY, INFINITY);
+                if (wid == 0) w_to_lds(B, lane, cur.x, cur.y);
                 __syncthreads();
                 const double A = B.cA[k], C = B.cC[k], q = B.cq[k];
                 double bl = k == 0 ? lo0 : lo, bh = k == 0 ? hi0 : hi;
@@ -2443,14 +2462,14 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     // the front stores each label's exact STATE x (not its key dx * x) and cost
     double2* fa = B.fa;
     double2* fb = B.fb;
-    if (lane == 0) fa[0] = make_double2(x0, 0.0);
+    if (tid == 0) fa[0] = make_double2(x0, 0.0);
     int n = 1;
     double xmin = x0, xmax = x0, cmin = 0.0, cmax = 0.0;    // state / cost range of the front
     const unsigned long long below = (1ull << lane) - 1ull;  // lanes < this one
-    for (int b = lane; b < NBK; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
+    for (int b = tid; b < NBK; b += NT) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
     // W_{k+1} of the stage in the LDS table, W_{k+2} in flight
     double2 wnext = make_double2(INFINITY, INFINITY);
-    if (prune) {
+    if (prune && wid == 0) {
         const double2 w1 = load_row(1);
         w_to_lds(B, lane, w1.x, w1.y);
         if (H >= 2) wnext = load_row(2);
@@ -2465,9 +2484,11 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             if (make_bound()) {
                 prune = true;
                 capn = CAPB;
-                const double2 wk = load_row(k + 1);
-                w_to_lds(B, lane, wk.x, wk.y);
-                wnext = k + 2 <= H ? load_row(k + 2) : make_double2(INFINITY, INFINITY);
+                if (wid == 0) {
+                    const double2 wk = load_row(k + 1);
+                    w_to_lds(B, lane, wk.x, wk.y);
+                    wnext = k + 2 <= H ? load_row(k + 2) : make_double2(INFINITY, INFINITY);
+                }
             }
             __syncthreads();
         }
@@ -2506,7 +2527,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         // 1. per key bucket the cheapest child (largest key among equally cheap ones), per
         //    cost bucket the largest-key child (cheapest among equal keys), both as
         //    understated bounds (cost up, key down), by 64-bit LDS atomics
-        for (int c = lane; c < nc && !nodom; c += WAVE) {
+        for (int c = tid; c < nc && !nodom; c += NT) {
             const int i = c / NU, u = c - i * NU;
             const double2 Li = fa[i];
             const double xc = fma(A, Li.x, fma(g, (double)u, C));
@@ -2522,7 +2543,7 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         // 2. mh[b] = min cost over the key buckets above b (lane l holds key chunk 63 - l:
         //    "above" = lower lanes, an exclusive prefix-min); kl[b] = max key over the cost
         //    buckets below b (lane l holds cost chunk l: an exclusive prefix-max)
-        if (!nodom) {
+        if (!nodom && wid == 0) {
             const int c0 = (WAVE - 1 - lane) * BPL, d0 = lane * BPL;
             unsigned bm[BPL], bk[BPL];
             unsigned lm = ~0u, lk = 0u;
@@ -2559,14 +2580,16 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         //    (the per-bucket tests need one strict inequality: X may be the reference)
         int nn = 0;
         unsigned kmn = ~0u, kmx = 0u, cmn = ~0u, cmx = 0u;  // survivors' fixed-point ranges
-        for (int c0 = 0; c0 < nc; c0 += WAVE) {
-            const int c = c0 + lane;
+        // child c of this stage: state, cost, fixed-point positions and the keep decision
+        auto eval = [&](int c, int& i, int& u, double& xc, double& cc, unsigned& vk, unsigned& vc) -> bool {
             const bool have = c < nc;
-            const int i = have ? c / NU : 0, u = c - i * NU;
+            i = have ? c / NU : 0;
+            u = c - i * NU;
             const double2 Li = fa[i];
-            const double xc = fma(A, Li.x, fma(g, (double)u, C));
-            const double cc = fma(q, (double)u, Li.y);
-            const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
+            xc = fma(A, Li.x, fma(g, (double)u, C));
+            cc = fma(q, (double)u, Li.y);
+            vk = fixp(fma(xc, kmul, kadd));
+            vc = fixp(fma(cc, csc, cadd));
             bool keep = have && xc >= bl && xc <= bh;
             if (keep && prune) keep = cc + w_eval(B, xc) <= UBT;
             if (keep && !nodom) {
@@ -2581,19 +2604,78 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
                 const bool d4 = ku <= zkd && cd >= zcu && (ku < zkd || cd > zcu);
                 keep = !(d1 || d2 || d3 || d4);
             }
-            const unsigned long long bal = __ballot(keep);
-            const int slot = nn + __popcll(bal & below);
-            nn += __popcll(bal);
-            if (keep && slot < capn) {
-                fb[slot] = make_double2(xc, cc);
-                B.par[k * PS + slot] = (uint16_t)(i | (u << 12));
-                kmn = umin(kmn, vk); kmx = umax(kmx, vk);
-                cmn = umin(cmn, vc); cmx = umax(cmx, vc);
+            return keep;
+        };
+        unsigned Kmn, Kmx, Cmn, Cmx;
+        if constexpr (NW == 1) {
+            for (int c0 = 0; c0 < nc; c0 += WAVE) {
+                int i, u;
+                double xc, cc;
+                unsigned vk, vc;
+                const bool keep = eval(c0 + lane, i, u, xc, cc, vk, vc);
+                const unsigned long long bal = __ballot(keep);
+                const int slot = nn + __popcll(bal & below);
+                nn += __popcll(bal);
+                if (keep && slot < capn) {
+                    fb[slot] = make_double2(xc, cc);
+                    B.par[k * PS + slot] = (uint16_t)(i | (u << 12));
+                    kmn = umin(kmn, vk); kmx = umax(kmx, vk);
+                    cmn = umin(cmn, vc); cmx = umax(cmx, vc);
+                }
+            }
+            Kmn = dpp_reduce(kmn, umin); Kmx = dpp_reduce(kmx, umax);
+            Cmn = dpp_reduce(cmn, umin); Cmx = dpp_reduce(cmx, umax);
+        } else {
+            // (a) each wave decides its contiguous passes, keeping the survivor masks; (b) after the
+            // exchange, each wave appends its survivors at its offset (the waves below it first)
+            const int P = (nc + WAVE - 1) / WAVE;
+            const int p0 = wid * P / NW, p1 = (wid + 1) * P / NW;
+            int cnt = 0;
+            for (int p = p0; p < p1; ++p) {
+                int i, u;
+                double xc, cc;
+                unsigned vk, vc;
+                const bool keep = eval(p * WAVE + lane, i, u, xc, cc, vk, vc);
+                const unsigned long long bal = __ballot(keep);
+                if (lane == 0) xmask[p] = bal;
+                cnt += __popcll(bal);
+                if (keep) { kmn = umin(kmn, vk); kmx = umax(kmx, vk); cmn = umin(cmn, vc); cmx = umax(cmx, vc); }
+            }
+            kmn = dpp_reduce(kmn, umin); kmx = dpp_reduce(kmx, umax);
+            cmn = dpp_reduce(cmn, umin); cmx = dpp_reduce(cmx, umax);
+            if (lane == 0) {
+                xint[0 * 8 + wid] = (unsigned)cnt; xint[1 * 8 + wid] = kmn; xint[2 * 8 + wid] = kmx;
+                xint[3 * 8 + wid] = cmn; xint[4 * 8 + wid] = cmx;
+            }
+            __syncthreads();
+            int off = 0;
+            Kmn = ~0u; Kmx = 0u; Cmn = ~0u; Cmx = 0u;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const int cw = (int)xint[w];
+                off += w < wid ? cw : 0;
+                nn += cw;
+                Kmn = umin(Kmn, xint[8 + w]); Kmx = umax(Kmx, xint[16 + w]);
+                Cmn = umin(Cmn, xint[24 + w]); Cmx = umax(Cmx, xint[32 + w]);
+            }
+            for (int p = p0; p < p1; ++p) {
+                const unsigned long long bal = xmask[p];
+                if ((bal >> lane) & 1ull) {
+                    const int c = p * WAVE + lane;
+                    const int i = c / NU, u = c - i * NU;
+                    const double2 Li = fa[i];
+                    const int slot = off + __popcll(bal & below);
+                    if (slot < capn) {
+                        fb[slot] = make_double2(fma(A, Li.x, fma(g, (double)u, C)), fma(q, (double)u, Li.y));
+                        B.par[k * PS + slot] = (uint16_t)(i | (u << 12));
+                    }
+                }
+                off += __popcll(bal);
             }
         }
 #ifdef DRAGG_FRONT_STATS
-        if (lane == 0) B.x[k * 8 + S_PAD] += (double)nn * (sx == S_T ? 1.0 : 1e4) +
-                                             (k == 0 ? (prune ? 1e8 : 0.0) * (sx == S_T ? 1.0 : 2.0) : 0.0);
+        if (tid == 0) B.x[k * 8 + S_PAD] += (double)nn * (sx == S_T ? 1.0 : 1e4) +
+                                            (k == 0 ? (prune ? 1e8 : 0.0) * (sx == S_T ? 1.0 : 2.0) : 0.0);
 #endif
         if (nn == 0) return 0;                       // no child left inside the feasible set
         if (nn > capn) return -3;                    // front overflow
@@ -2601,8 +2683,6 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
         // position V of a value lies in [v - 1, v + 2], widened past the back-conversion's
         // rounding
         {
-            const unsigned Kmn = dpp_reduce(kmn, umin), Kmx = dpp_reduce(kmx, umax);
-            const unsigned Cmn = dpp_reduce(cmn, umin), Cmx = dpp_reduce(cmx, umax);
             const double klo = dx > 0.0 ? xl : -xh;
             const double ik = (xh - xl) * (1.0 / FX);     // ~1 / ksc; tw() covers the difference
             const double k1 = fma((double)Kmn - 1.0, ik, klo), k2 = fma((double)Kmx + 2.0, ik, klo);
@@ -2614,8 +2694,8 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
             cmin = c1 - tw(c1);
             cmax = c2 + tw(c2);
         }
-        for (int b = lane; b < NBK && !nodom; b += WAVE) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
-        if (prune && k + 1 < H) {
+        for (int b = tid; b < NBK && !nodom; b += NT) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
+        if (prune && k + 1 < H && wid == 0) {
             w_to_lds(B, lane, wnext.x, wnext.y);
             if (k + 3 <= H) wnext = load_row(k + 3);
         }
@@ -2626,15 +2706,26 @@ DEV int dp_front(const FrontBufs& B, int H, int lane, double g, double x0, doubl
     // the cheapest final label (lowest index on ties)
     double best = INFINITY;
     int bi = -1;
-    for (int i = lane; i < n; i += WAVE)
+    for (int i = tid; i < n; i += NT)
         if (fa[i].y < best) { best = fa[i].y; bi = i; }
     for (int o = 32; o > 0; o >>= 1) {
         const double ob = __shfl_xor(best, o);
         const int oi = __shfl_xor(bi, o);
         if (ob < best || (ob == best && oi >= 0 && (bi < 0 || oi < bi))) { best = ob; bi = oi; }
     }
+    if constexpr (NW > 1) {
+        if (lane == 0) { xbest[wid] = best; xint[wid] = (unsigned)bi; }
+        __syncthreads();
+        best = xbest[0]; bi = (int)xint[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) {
+            const double ob = xbest[w];
+            const int oi = (int)xint[w];
+            if (ob < best || (ob == best && oi >= 0 && (bi < 0 || oi < bi))) { best = ob; bi = oi; }
+        }
+    }
     if (best_out) *best_out = best;
-    if (lane == 0) {
+    if (tid == 0) {
         int j = bi;
         for (int k = H - 1; k >= 0; --k) {
             const int p = B.par[k * PS + j];
@@ -2670,6 +2761,7 @@ DEV bool round_duties(const Home& h, const Lds& L, int lane, uint16_t* par) {
     B.fhi = reinterpret_cast<unsigned*>(f); f += (H + 2) / 2;
     B.cA = cA; B.cC = cC; B.cq = cq; B.x = L.x; B.par = par;
     B.wg = nullptr; B.wlx = B.wlv = B.wls = nullptr;     // no bound pruning on this path
+    B.xch = nullptr;                                     // one wave
     const bool front = h.S == 6 && par != nullptr && (f - L.Lf) <= 128 * H;
     for (int k = lane; k < H; k += WAVE) {
         cA[k] = h.aT;
@@ -2830,9 +2922,10 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
 // bucketed DP and the big pass out of DM_FRONT keeps their registers and LDS out of the hot kernel.
 enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1 };
 
-template <bool EXPLICIT, int MODE>
+template <bool EXPLICIT, int MODE, int NW = 1>
 DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int first_chain) {
-    constexpr int NT = WAVE;
+    static_assert(NW == 1 || MODE == DM_FRONT, "several waves per home in the hot launch only");
+    constexpr int NT = NW * WAVE;
     const int lane = threadIdx.x;
     const int N = a.d.n_homes;
     const int H = a.d.horizon;
@@ -2889,8 +2982,8 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
         // 10,000): the hot launch hands these homes to the second one right away, which prunes
         // with the LP bound.  (Pruning by bound at every tariff boundary too: -14 % latency of
         // the slowest homes over the first 48 steps of the bench, but +13 % time over all 96.)
-        int changes = 0;
-        for (int k = lane; k < H; k += NT) changes += (k > 0 && D.price[k] != D.price[k - 1]) ? 1 : 0;
+        int changes = 0;                              // (every wave counts all stages)
+        for (int k = lane & (WAVE - 1); k < H; k += WAVE) changes += (k > 0 && D.price[k] != D.price[k - 1]) ? 1 : 0;
         changes = dpp_isum(changes);
         const bool rl_prices = changes * 4 > H;
         const bool use_bound = rl_prices;
@@ -2931,9 +3024,11 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
             if (h.S == 6 && !(MODE == DM_BUCKET && rl_prices)) {
                 double* const wl = D.wl;
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
-                                   wg, wl, wl + WAVE, wl + 2 * WAVE};
-                r = MODE == DM_FRONT ? dp_front<6, NF_HOT, NF_HOT, NB_CAP, NTB_HOT>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound)
-                                     : dp_front<6, NF, NF_BOUND>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
+                                   wg, wl, wl + WAVE, wl + 2 * WAVE, MODE == DM_FRONT ? D.xch : nullptr};
+                if constexpr (MODE == DM_FRONT)
+                    r = dp_front<6, NF_HOT, NF_HOT, NB_CAP, NTB_HOT, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
+                else
+                    r = dp_front<6, NF, NF_BOUND>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
 #ifdef DRAGG_FRONT_STATS2
                 // diagnostic: the T chain's fronts when the bound is the optimum itself
                 if (c0 && r == 1 && use_bound) {
@@ -3020,11 +3115,11 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
         for (int k = 0; k < DRAGG_NPHASE; ++k) a.out.cycles[(size_t)k * N + home] = (int64_t)pf.acc[k];
 }
 
-template <bool EXPLICIT, int MODE>
-__global__ __launch_bounds__(WAVE, MODE == DM_FRONT ? 3 : 2) void mpc_direct_kernel(KArgs a) {
+template <bool EXPLICIT, int MODE, int NW = 1>
+__global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : 2) void mpc_direct_kernel(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     if (MODE == DM_FRONT) {
-        if ((int)blockIdx.x < a.d.n_homes) solve_direct<EXPLICIT, MODE>(a, blockIdx.x, smem, 0, 0);
+        if ((int)blockIdx.x < a.d.n_homes) solve_direct<EXPLICIT, MODE, NW>(a, blockIdx.x, smem, 0, 0);
         return;
     }
     // persistent: block b solves the deferred homes b, b + gridDim.x, ... of the list (its own
@@ -3119,9 +3214,37 @@ int launch_kernel(K kern, int& attr_state, const KArgs& a, int blocks, int nt, s
 // hipFuncSetAttribute is per device: the attribute state is kept per device (a process driving
 // several GPUs sets it once on each)
 constexpr int MAX_DEV = 64;
+
+// Waves per home of the hot launch.  With more homes than the GPU holds at once, one wave per home
+// (throughput: a SIMD interleaves 3 homes).  With few homes (a strong-scaling shard) every home is
+// resident anyway and the step time is the slowest home's latency: 2 or 4 waves then split each
+// DP stage's children (bit-identical results).  DRAGG_WAVES_PER_HOME=1|2|4 forces a choice
+// (diagnostic, A/B runs).
+template <bool EXPLICIT>
+int hot_waves(int N, int dev, size_t lds) {
+    const char* env = getenv("DRAGG_WAVES_PER_HOME");
+    if (env && (env[0] == '1' || env[0] == '2' || env[0] == '4') && env[1] == 0) return env[0] - '0';
+    static int cap_dev[MAX_DEV][3] = {};                 // resident homes at 1, 2, 4 waves per home
+    if (!cap_dev[dev][0]) {
+        hipDeviceProp_t prop{};
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 1;
+        const void* k[3] = {(const void*)mpc_direct_kernel<EXPLICIT, DM_FRONT, 1>,
+                            (const void*)mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>,
+                            (const void*)mpc_direct_kernel<EXPLICIT, DM_FRONT, 4>};
+        for (int i = 0; i < 3; ++i) {
+            int per_cu = 0;
+            if (hipFuncSetAttribute(k[i], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k[i], WAVE << i, lds) != hipSuccess)
+                return 1;
+            cap_dev[dev][i] = max(1, per_cu * prop.multiProcessorCount);
+        }
+    }
+    return N <= cap_dev[dev][2] ? 4 : N <= cap_dev[dev][1] ? 2 : 1;
+}
+
 template <bool EXPLICIT>
 int launch(const KArgs& a, hipStream_t s) {
-    static int attr_dev[MAX_DEV][4] = {};
+    static int attr_dev[MAX_DEV][6] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return DRAGG_E_HIP;
     int* const attr = attr_dev[dev];
@@ -3131,7 +3254,11 @@ int launch(const KArgs& a, hipStream_t s) {
     // the deferred list starts empty (its length word), then the hot launch, then the second
     int* const len = reinterpret_cast<int*>(reinterpret_cast<char*>(a.p.workspace) + defer_offset(N, a.d.horizon)) + N;
     if (hipMemsetAsync(len, 0, sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
-    const int rc = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT>, attr[1], a, N, WAVE, kernel_lds_bytes(&a.d), s);
+    const size_t lds = kernel_lds_bytes(&a.d);
+    const int nw = hot_waves<EXPLICIT>(N, dev, lds);
+    const int rc = nw == 4 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 4>, attr[4], a, N, 4 * WAVE, lds, s)
+                 : nw == 2 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>, attr[3], a, N, 2 * WAVE, lds, s)
+                           : launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 1>, attr[1], a, N, WAVE, lds, s);
     if (rc) return rc;
     return launch_kernel(mpc_direct_kernel<EXPLICIT, DM_BUCKET>, attr[2], a, min(N, SECOND_SLOTS), WAVE,
                          (size_t)big_layout(a.d.horizon, a.d.sub_steps).bytes, s);

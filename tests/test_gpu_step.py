@@ -208,3 +208,34 @@ def test_ecos_solver_every_solve_falls_back(gpu):
             status, _, _ = M.run_home_step(hcs[i], t, hashes[i], oenv, noise[:, i], solver=raises)
             assert status is None and st[i] == L.ST_SOLVER_ERROR, (h["name"], t, st[i])
             assert b.hash_dict(i) == hashes[i], (h["name"], t)
+
+
+def test_waves_per_home_bit_identical(gpu):
+    """The hot launch's waves per home (1 for throughput; 2 or 4 when the homes all fit on the GPU
+    at once, a strong-scaling shard) split each DP stage's children over the waves but keep the
+    single-wave order: 12 closed-loop steps of 1,500 homes of the bench community (H = 48, July,
+    TOU: tariff boundaries, LP-bound pruning) give the same hash, status and objective bit for bit."""
+    import math
+    import os
+    import torch
+    from dragg_amd.aggregator import DeviceAggregator
+    from dragg_amd.community import synthetic_homes, synthetic_weather
+    steps, dt, hh = 12, 4, 12
+    days = math.ceil((math.ceil(steps / dt) + hh + 2) / 24) + 1
+    homes = synthetic_homes(1500, seed=12, days=days, dt=dt, horizon_hours=hh)
+    oat, ghi, tou = synthetic_weather(days, dt, math.ceil(steps / dt), seed=3, month=7)
+    out = {}
+    try:
+        for nw in ("1", "2", "4"):
+            os.environ["DRAGG_WAVES_PER_HOME"] = nw
+            agg = DeviceAggregator(homes, oat, ghi, tou, 0, steps, reward_price=[0.0], seed=12)
+            for t in range(steps):
+                agg.run_iteration()
+            torch.cuda.synchronize()
+            out[nw] = (agg.hist.nan_to_num(7.5).cpu(), agg.batch.fc.nan_to_num(7.5).cpu(), agg.status_hist.cpu(),
+                       agg.batch.obj.nan_to_num(7.5).cpu())
+    finally:
+        os.environ.pop("DRAGG_WAVES_PER_HOME", None)
+    for nw in ("2", "4"):
+        for a, b in zip(out["1"], out[nw]):
+            assert torch.equal(a, b), nw

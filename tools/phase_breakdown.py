@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--int-mode", default="round")
     ap.add_argument("--month", type=int, default=1)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--world", type=int, default=1, help="rank 0's strided shard of a community sharded this wide")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -34,7 +35,7 @@ def main():
     homes = synthetic_homes(a.homes, seed=12, days=days, dt=a.dt, horizon_hours=a.horizon_hours)
     oat, ghi, tou = synthetic_weather(days, a.dt, sim_hours, seed=3, month=a.month)
     agg = DeviceAggregator(homes, oat, ghi, tou, 0, a.steps, reward_price=[0.0], int_mode=a.int_mode,
-                           seed=12, keep_history=False)
+                           seed=12, keep_history=False, rank=0, world=a.world)
     agg.batch.enable_phase_timing(True)
     cyc, st, it, kms = [], [], [], []
     for _ in range(a.steps):
@@ -42,7 +43,7 @@ def main():
         e0.record()
         agg.run_iteration()
         e1.record()
-        agg.collect_data()
+        agg.collect_data(defer=True)
         torch.cuda.synchronize()
         kms.append(e0.elapsed_time(e1))
         cyc.append(agg.batch.cycles.cpu().numpy().copy())
@@ -65,6 +66,13 @@ def main():
     res["slowest_home"] = {"step": int(t_i), "home": int(h_i), "type": int(agg.batch.types_host[h_i]),
                            "status": int(st[t_i, h_i]), "iters": int(it[t_i, h_i])}
     res["per_step_max_over_mean"] = float(np.mean(tot.max(1) / tot.mean(1)))
+    # the step's slowest home (sets the launch time when homes < resident slots): its phase split
+    slow = np.argmax(tot, axis=1)
+    res["step_slowest_phase_share"] = {name: float(np.mean([cyc[t, p, slow[t]] / tot[t, slow[t]]
+                                                            for t in range(a.steps)])) for p, name in enumerate(L.PHASES)}
+    res["step_slowest_type_counts"] = np.bincount(agg.batch.types_host[slow], minlength=4).tolist()
+    res["step_max_cycles_pct"] = {str(q): float(np.percentile(tot.max(1), q)) for q in (10, 50, 90)}
+    res["kernel_ms_per_step"] = [round(x, 4) for x in kms]
     res["iters_pct"] = {str(q): float(np.percentile(it, q)) for q in (50, 90, 99, 100)}
     res["status_counts"] = {n: int((st == i).sum()) for i, n in enumerate(L.STATUS_NAMES)}
     by_type = {}
