@@ -37,6 +37,7 @@ K = {k: i for i, k in enumerate(VAL_KEYS)}
 PATH_APPROX_MASK = 0xFFF
 PATH_SECOND = 1 << 12
 PATH_FAIL_T, PATH_FAIL_TW = 1 << 13, 1 << 14     # ROUND_FAIL decided by the indoor-air / tank chain
+PATH_STEPS = 1 << 15           # solved by the exact step-function DP (DM_NARROW launch)
 STATUS_NAMES = ["optimal", "infeasible", "infeasible_cert", "max_iter", "round_fail", "err_parse",
                 "err_missing", "solver_error"]
 

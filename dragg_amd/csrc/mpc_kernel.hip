@@ -43,6 +43,9 @@ constexpr int NTB_HOT = 64;           // key / cost buckets per stage of the hot
                                       //   (small fronts: a one-bucket-per-lane scan; measured 128: +6 % time)
 constexpr int NTB = 192;              // ... of the second launch's regular front DP and round_lp
 constexpr int NTB_BIG = 256;          // ... of the big exact pass (fronts up to NF_BIG)
+constexpr int NT_STEPS = 1024;           // threads of a DM_NARROW block
+constexpr int STEP_CAP = 16384;          // breakpoints per value function
+constexpr int NARROW_SLOTS = 8;          // blocks of the persistent DM_NARROW launch
 // exchange area of a multi-wave front DP: per-pass survivor masks, per-wave counts / ranges / minima
 constexpr int XCH_PASSES = 32;
 constexpr int XCH_BYTES = XCH_PASSES * 8 + 8 * 8 + 8 * 5 * 4;
@@ -1186,6 +1189,7 @@ struct KArgs {
     dragg_mpc_out out;
     const double* noise;
     int t;
+    int force_steps;       // diagnostic (DRAGG_FORCE_STEP_DP=1): every home to the exact step DP
 };
 
 // --------------------------------------------------------------------------------------
@@ -1440,6 +1444,22 @@ __host__ __device__ inline size_t big_region_offset(int N, int H) {
     return (w_region_offset(N, H) + w_region_bytes(N, H) + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t big_region_bytes(int H) { return (size_t)SECOND_SLOTS * H * NF_BIG * sizeof(uint16_t); }
+// then the list of homes the second launch hands to DM_NARROW ([N] i32 + its length) and
+// (256-aligned) DM_NARROW's step-function storage, one region per block of that launch
+__host__ __device__ inline size_t step_slot_bytes(int H) {
+    // V_k breakpoints and values [H + 1][STEP_CAP] f64 each, merged candidates and interval values
+    // [(16)(STEP_CAP + 1)] f64 each (S <= 15)
+    return ((size_t)2 * (H + 1) * STEP_CAP + (size_t)2 * 16 * (STEP_CAP + 1)) * sizeof(double);
+}
+__host__ __device__ inline size_t narrow_list_offset(int N, int H) {
+    return (big_region_offset(N, H) + big_region_bytes(H) + 255) / 256 * 256;
+}
+__host__ __device__ inline size_t narrow_region_offset(int N, int H) {
+    return (narrow_list_offset(N, H) + (size_t)(N + 1) * sizeof(int) + 255) / 256 * 256;
+}
+__host__ __device__ inline size_t direct_workspace_bytes(int N, int H) {
+    return narrow_region_offset(N, H) + (size_t)NARROW_SLOTS * step_slot_bytes(H);
+}
 
 struct DirectLayout {
     int draw, oat, ghi, price, cA, cC, cq, sc, t2, bx0, bp1, bp2, lab, rmin, tail;
@@ -1531,6 +1551,21 @@ __host__ __device__ inline DirectLayout direct_layout(int H, int S) {
 }
 
 __host__ __device__ inline int direct_lds_bytes(int H, int S) { return direct_layout(H, S).bytes; }
+
+// DM_NARROW: the direct layout, then the step DP's LDS: counts [H + 1] i32, scan scratch, the
+// reachable hull [2][H + 1] f64
+struct NarrowLayout { int cnt, red, rl, rh, bytes; };
+__host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
+    NarrowLayout o{};
+    int p = direct_layout(H, S).bytes;
+    auto take = [&](int bytes, int align) { p = (p + align - 1) / align * align; const int r = p; p += bytes; return r; };
+    o.cnt = take(4 * (H + 1), 4);
+    o.red = take(4 * (NT_STEPS / 64 + 2), 4);
+    o.rl = take(8 * (H + 1), 8);
+    o.rh = take(8 * (H + 1), 8);
+    o.bytes = (p + 15) / 16 * 16;
+    return o;
+}
 
 // The second launch: the direct layout, and over its DP arrays (from lab on; the bucketed DP
 // is done with them, its schedule is in the global solution array) the big exact pass's
@@ -2910,6 +2945,217 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
     return true;
 }
 
+// --------------------------------------------------------------------------------------
+// EXACT thermal chain DP without any dominance assumption: backward step functions (dp_steps).
+//
+// The front DP's dominance needs every feasible set F_k at least one duty step wide (and prices
+// of one sign); a tank whose feasible window narrows below one duty step (a large draw ahead)
+// breaks it (measured: the bucketed approximation then misses the optimum by up to 8.5 %).  This
+// DP assumes nothing: V_k(x) = min_u q_k u + V_{k+1}(A_k x + C_k + g u) is piecewise CONSTANT in
+// x, carried backward as sorted breakpoints and values (+inf where no schedule exists), the
+// reference's MILP optimum recovered forward by evaluating V_{k+1} at the exact successor
+// states -- the algorithm of the CPU oracle (oracle/thermal.py), restricted to the states the
+// chain can reach from x_0 (a forward interval hull).  Such V_k can hold thousands of breakpoints
+// (up to ~9k measured on narrow tanks), so it runs on a 1,024-thread block of its own launch
+// (DM_NARROW): per stage the (S+1) shifted breakpoint lists are merged by rank (binary searches),
+// each elementary interval's value taken at its midpoint, and equal neighbours compacted by block
+// scans; the V_k live in the workspace.  Returns 1 solved, 0 no integer schedule, -3 a V_k past
+// STEP_CAP breakpoints (the caller keeps its bucketed schedule).
+// --------------------------------------------------------------------------------------
+
+
+// exclusive prefix sum over the NT threads of the block (red: >= NT/64 + 1 ints of LDS); also
+// returns the total in *tot
+template <int NT>
+DEV int block_excl_scan(int v, int* red, int tid, int* tot) {
+    const int lane = tid & (WAVE - 1), w = tid / WAVE;
+    const int inc = dpp_iscan(v, lane, 0, [](int a, int b) { return a + b; });
+    __syncthreads();
+    if (lane == WAVE - 1) red[w] = inc;
+    __syncthreads();
+    int off = 0, all = 0;
+#pragma unroll
+    for (int i = 0; i < NT / WAVE; ++i) {
+        const int r = red[i];
+        off += i < w ? r : 0;
+        all += r;
+    }
+    *tot = all;
+    return off + inc - v;
+}
+
+struct StepBufs {
+    double* VB;                  // [H + 1][STEP_CAP] breakpoints of V_k
+    double* VV;                  // [H + 1][STEP_CAP] values of V_k on [B_i, B_{i+1})
+    double* cand;                // [(S + 1)(STEP_CAP + 1)] merged candidate points
+    double* ival;                // [(S + 1)(STEP_CAP + 1) + 1] elementary-interval values
+    int* cnt;                    // LDS [H + 1] breakpoints of V_k (m + 1 points, m values)
+    int* red;                    // LDS [NT / 64 + 1] scan scratch
+    double* rl;                  // LDS [H + 1] reachable hull of x_k (widened)
+    double* rh;
+};
+
+template <int NT>
+DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const double* cq, int H, int S, double g,
+                 double x0, double lo0, double hi0, double lo, double hi, double* X, int sx, int sv, int tid) {
+    auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
+    auto boxlo = [&](int k) { const double b = k == 0 ? lo0 : lo; return b - tw(b); };   // box of x_{k+1}
+    auto boxhi = [&](int k) { const double b = k == 0 ? hi0 : hi; return b + tw(b); };
+    // forward reachable hull R_{k+1} of x_{k+1} (interval arithmetic, widened past rounding)
+    if (tid == 0) {
+        double l = x0, u = x0;
+        const double gmin = fmin(0.0, g * S), gmax = fmax(0.0, g * S);
+        Sb.rl[0] = x0; Sb.rh[0] = x0;
+        for (int k = 0; k < H; ++k) {
+            double a = cA[k] * l + cC[k] + gmin, b = cA[k] * u + cC[k] + gmax;
+            a -= tw(a); b += tw(b);
+            l = fmax(a, boxlo(k)); u = fmin(b, boxhi(k));
+            Sb.rl[k + 1] = l; Sb.rh[k + 1] = u;
+        }
+    }
+    __syncthreads();
+    for (int k = 1; k <= H; ++k)
+        if (!(Sb.rl[k] <= Sb.rh[k])) return 0;            // no state of stage k stays in its box
+    // V_H = 0 on its domain
+    double* const VB = Sb.VB;
+    double* const VV = Sb.VV;
+    if (tid == 0) {
+        VB[(size_t)H * STEP_CAP + 0] = Sb.rl[H];
+        VB[(size_t)H * STEP_CAP + 1] = Sb.rh[H];
+        VV[(size_t)H * STEP_CAP + 0] = 0.0;
+        Sb.cnt[H] = 1;
+    }
+    __syncthreads();
+    const int NU = S + 1;
+    for (int k = H - 1; k >= 1; --k) {
+        const double A = cA[k], C = cC[k], q = cq[k];
+        const double iA = 1.0 / A;
+        const double* B = VB + (size_t)(k + 1) * STEP_CAP;
+        const double* V = VV + (size_t)(k + 1) * STEP_CAP;
+        const int m = Sb.cnt[k + 1];                     // values; m + 1 breakpoints
+        const int np = m + 1;
+        auto P = [&](int u, int i) { return (B[i] - C - g * (double)u) * iA; };     // preimage points
+        // number of points of list u below p (or <= p)
+        auto below = [&](int u, double p, bool le) {
+            int a = 0, b = np;
+            while (a < b) {
+                const int c = (a + b) >> 1;
+                const double v = P(u, c);
+                if (le ? v <= p : v < p) a = c + 1; else b = c;
+            }
+            return a;
+        };
+        // (1) merge the NU lists by rank (ties: lower duty first, then lower index)
+        const int Mc = NU * np;
+        for (int idx = tid; idx < Mc; idx += NT) {
+            const int u = idx / np, i = idx - u * np;
+            const double p = P(u, i);
+            int r = i;
+            for (int u2 = 0; u2 < NU; ++u2)
+                if (u2 != u) r += below(u2, p, u2 < u);
+            Sb.cand[r] = p;
+        }
+        __syncthreads();
+        // (2) elementary intervals of the domain D_k = box of x_k and reachable hull
+        const double dl = fmax(boxlo(k - 1), Sb.rl[k]), dh = fmin(boxhi(k - 1), Sb.rh[k]);
+        if (!(dl <= dh)) return 0;
+        int jl, jh;                                       // candidates strictly inside (dl, dh)
+        {
+            int a = 0, b = Mc;
+            while (a < b) { const int c = (a + b) >> 1; if (Sb.cand[c] <= dl) a = c + 1; else b = c; }
+            jl = a;
+            a = jl; b = Mc;
+            while (a < b) { const int c = (a + b) >> 1; if (Sb.cand[c] < dh) a = c + 1; else b = c; }
+            jh = a;
+        }
+        const int T = jh - jl + 1;                        // intervals [e_t, e_{t+1})
+        // (3) each interval's value at its midpoint; NaN marks a zero-width interval
+        for (int t = tid; t < T; t += NT) {
+            const double e0 = t == 0 ? dl : Sb.cand[jl + t - 1];
+            const double e1 = t == T - 1 ? dh : Sb.cand[jl + t];
+            double best = NAN;
+            if (e1 > e0) {
+                const double mid = 0.5 * (e0 + e1);
+                best = INFINITY;
+                for (int u = 0; u < NU; ++u) {
+                    const int i = below(u, mid, true) - 1;       // interval of list u holding mid
+                    if (i >= 0 && i < m) best = fmin(best, fma(q, (double)u, V[i]));
+                }
+            }
+            Sb.ival[t] = best;
+        }
+        __syncthreads();
+        // (4) compaction: drop zero-width intervals, then merge equal neighbours (two block scans
+        //     over contiguous per-thread chunks, so that order is kept)
+        const int per = (T + NT - 1) / NT;
+        const int t0 = min(T, tid * per), t1 = min(T, t0 + per);
+        int c1 = 0;
+        for (int t = t0; t < t1; ++t) c1 += Sb.ival[t] == Sb.ival[t] ? 1 : 0;
+        int tot1;
+        int o1 = block_excl_scan<NT>(c1, Sb.red, tid, &tot1);
+        // the nonzero-width intervals (start, value) into cand[jh + 1 ...] (cand[0 .. jh) still read:
+        // starts), via a second array region: ival holds values, cand beyond Mc is free
+        double* const ks = Sb.cand + Mc;                  // kept starts  [T] (cand has 16 (cap+1) slots)
+        double* const kv = Sb.ival + T;                   // kept values  [T]
+        for (int t = t0; t < t1; ++t) {
+            const double v = Sb.ival[t];
+            if (v == v) {
+                ks[o1] = t == 0 ? dl : Sb.cand[jl + t - 1];
+                kv[o1] = v;
+                ++o1;
+            }
+        }
+        __syncthreads();
+        if (tot1 == 0) return 0;
+        const int per2 = (tot1 + NT - 1) / NT;
+        const int s0 = min(tot1, tid * per2), s1 = min(tot1, s0 + per2);
+        int c2 = 0;
+        for (int j = s0; j < s1; ++j) c2 += (j == 0 || kv[j] != kv[j - 1]) ? 1 : 0;
+        int tot2;
+        int o2 = block_excl_scan<NT>(c2, Sb.red, tid, &tot2);
+        if (tot2 + 1 > STEP_CAP) return -3;
+        double* const OB = VB + (size_t)k * STEP_CAP;
+        double* const OV = VV + (size_t)k * STEP_CAP;
+        for (int j = s0; j < s1; ++j)
+            if (j == 0 || kv[j] != kv[j - 1]) { OB[o2] = ks[j]; OV[o2] = kv[j]; ++o2; }
+        if (tid == 0) { OB[tot2] = dh; Sb.cnt[k] = tot2; }
+        __syncthreads();
+    }
+    // forward recovery (wave 0: duty u on lane u): the cheapest q u + V_{k+1}(x') over the
+    // duties whose successor stays in its box, lowest duty on ties (the oracle's rule)
+    bool ok = true;
+    if (tid < WAVE) {
+        const int lane = tid;
+        double x = x0;
+        for (int k = 0; k < H && ok; ++k) {
+            const double xn = fma(cA[k], x, fma(g, (double)lane, cC[k]));
+            double val = INFINITY;
+            if (lane <= S && xn >= boxlo(k) && xn <= boxhi(k)) {
+                if (k + 1 < H) {
+                    const double* B = VB + (size_t)(k + 1) * STEP_CAP;
+                    const double* V = VV + (size_t)(k + 1) * STEP_CAP;
+                    const int m = Sb.cnt[k + 1];
+                    if (xn >= B[0] && xn <= B[m]) {
+                        int a = 0, b = m + 1;
+                        while (a < b) { const int c = (a + b) >> 1; if (B[c] <= xn) a = c + 1; else b = c; }
+                        val = fma(cq[k], (double)lane, V[min(a - 1, m - 1)]);
+                    }
+                } else {
+                    val = cq[k] * (double)lane;
+                }
+            }
+            const double vm = dpp_reduce(val, [](double a, double b) { return fmin(a, b); });
+            if (!(vm < INFINITY)) { ok = false; break; }
+            const int bu = __ffsll((long long)__ballot(val == vm)) - 1;
+            x = read_lane(xn, bu);
+            if (lane == 0) { X[k * 8 + sv] = (double)bu; X[k * 8 + sx] = x; }
+        }
+        if (lane == 0) Sb.cnt[0] = ok ? 1 : 0;
+    }
+    __syncthreads();
+    return Sb.cnt[0];
+}
+
 // The direct path is two launches.  DM_FRONT (the hot one, one block per home) runs the exact
 // front DP with fronts of up to NF labels (NF_BOUND with the LP bound).  A home where it does not
 // apply (front overflow -- stage-varying RL prices --, mixed-sign prices, a too-narrow feasible set,
@@ -2920,17 +3166,18 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
 // labels (its own back-pointer rows per block), which replaces that schedule by the optimum.  Only
 // a chain that outgrows even NF_BIG keeps the bucketed schedule (int_path records it).  Keeping the
 // bucketed DP and the big pass out of DM_FRONT keeps their registers and LDS out of the hot kernel.
-enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1 };
+enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1, DM_NARROW = 2 };
 
 template <bool EXPLICIT, int MODE, int NW = 1>
 DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int first_chain) {
-    static_assert(NW == 1 || MODE == DM_FRONT, "several waves per home in the hot launch only");
+    static_assert(NW == 1 || MODE != DM_BUCKET, "one wave per home in the second launch");
     constexpr int NT = NW * WAVE;
     const int lane = threadIdx.x;
     const int N = a.d.n_homes;
     const int H = a.d.horizon;
     char* const ws = reinterpret_cast<char*>(a.p.workspace);
     int* const list = reinterpret_cast<int*>(ws + defer_offset(N, H));     // [N] + length at [N]
+    int* const nlist = reinterpret_cast<int*>(ws + narrow_list_offset(N, H));   // DM_BUCKET -> DM_NARROW
     Home h;
     LdsD D = MODE == DM_FRONT ? carve_front(smem, H) : carve_direct(smem, H, a.d.sub_steps);
     D.par = reinterpret_cast<uint16_t*>(ws) + (size_t)home * H * NB_CAP;
@@ -2987,6 +3234,10 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
         changes = dpp_isum(changes);
         const bool rl_prices = changes * 4 > H;
         const bool use_bound = rl_prices;
+        if (MODE == DM_FRONT && a.force_steps) {
+            if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home;
+            return;
+        }
         if (MODE == DM_FRONT && rl_prices) {
             if (lane == 0) list[atomicAdd(list + N, 1)] = home;
             return;
@@ -3021,6 +3272,27 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
             // prices, a feasible set narrower than one duty step, front overflow, S != 6)
             int r = -5;                                    // reason 5: the exact DP not run (S != 6)
             double2* const wg = reinterpret_cast<double2*>(ws + w_region_offset(N, H)) + (size_t)home * (H + 1) * WAVE;
+            if constexpr (MODE == DM_NARROW) {
+                // the exact step-function DP (any prices, any feasible sets); past its capacity the
+                // bucketed DP's schedule is kept (reason 6)
+                const NarrowLayout nl = narrow_layout(H, a.d.sub_steps);
+                char* const sb = reinterpret_cast<char*>(smem);
+                double* const sw = reinterpret_cast<double*>(ws + narrow_region_offset(N, H) + (size_t)slot * step_slot_bytes(H));
+                const StepBufs SB{sw, sw + (size_t)(H + 1) * STEP_CAP, sw + (size_t)2 * (H + 1) * STEP_CAP,
+                                  sw + (size_t)2 * (H + 1) * STEP_CAP + (size_t)16 * (STEP_CAP + 1),
+                                  reinterpret_cast<int*>(sb + nl.cnt), reinterpret_cast<int*>(sb + nl.red),
+                                  reinterpret_cast<double*>(sb + nl.rl), reinterpret_cast<double*>(sb + nl.rh)};
+                r = dp_steps<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, D.x, sx, sv, lane);
+                if (r >= 0) {
+                    ok = r == 1;
+                } else {
+                    ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
+                                  : dp_thermal<0>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
+                    int_path |= (1 << chain) | (6 << (4 + 4 * chain));
+                }
+                if (!ok) int_path |= 1 << (13 + chain);
+                continue;
+            }
             if (h.S == 6 && !(MODE == DM_BUCKET && rl_prices)) {
                 double* const wl = D.wl;
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
@@ -3044,6 +3316,11 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 ok = r == 1;
             } else if (MODE == DM_FRONT) {                 // leave the home to DM_BUCKET
                 if (lane == 0) list[atomicAdd(list + N, 1)] = home | (chain << 30);
+                return;
+            } else if (r == -1 || r == -2 || (r == -5 && !rl_prices)) {
+                // no dominance here (mixed-sign prices without a usable bound, a feasible set
+                // narrower than one duty step, S != 6): the exact step-function DP of DM_NARROW
+                if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30);
                 return;
             } else {
                 ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
@@ -3075,6 +3352,10 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                     if (r2 == 1) ok = true;
                     else if (r2 == 0 && !ok) ok = false;      // exact: no integer schedule
                     else if (r2 == 0) r2 = -4;                // bound inconsistent with the schedule: keep it
+                    if (r2 < 0) {                             // past NF_BIG: the exact step-function DP
+                        if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30);
+                        return;
+                    }
                 }
                 if (r2 < 0) int_path |= (1 << chain) | ((-r2) << (4 + 4 * chain));   // chain bit + reason
             }
@@ -3106,7 +3387,8 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
         a.out.iters[home] = 0;
         a.out.obj[home] = obj;
         a.out.relax_obj[home] = NAN;
-        if (a.out.int_path) a.out.int_path[home] = int_path | (MODE == DM_BUCKET ? (1 << 12) : 0);
+        if (a.out.int_path)
+            a.out.int_path[home] = int_path | (MODE != DM_FRONT ? (1 << 12) : 0) | (MODE == DM_NARROW ? (1 << 15) : 0);
     }
     if (a.out.hist && lane == 0)      // lane 0 wrote every vals field of this home
         for (int k = 0; k < DRAGG_NVAL; ++k) a.out.hist[(size_t)k * N + home] = io.v(k);
@@ -3116,22 +3398,23 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
 }
 
 template <bool EXPLICIT, int MODE, int NW = 1>
-__global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : 2) void mpc_direct_kernel(KArgs a) {
+__global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_BUCKET ? 2 : 1) void mpc_direct_kernel(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     if (MODE == DM_FRONT) {
         if ((int)blockIdx.x < a.d.n_homes) solve_direct<EXPLICIT, MODE, NW>(a, blockIdx.x, smem, 0, 0);
         return;
     }
-    // persistent: block b solves the deferred homes b, b + gridDim.x, ... of the list (its own
-    // back-pointer rows: slot b); every block reaches the end of the list and exits
+    // persistent: block b solves the listed homes b, b + gridDim.x, ... (its own scratch rows in
+    // the workspace: slot b); every block reaches the end of the list and exits
     const int* const list = reinterpret_cast<const int*>(reinterpret_cast<const char*>(a.p.workspace) +
-                                                         defer_offset(a.d.n_homes, a.d.horizon));
+                                                         (MODE == DM_BUCKET ? defer_offset(a.d.n_homes, a.d.horizon)
+                                                                            : narrow_list_offset(a.d.n_homes, a.d.horizon)));
     const int cnt = min(list[a.d.n_homes], a.d.n_homes);
     for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
         const int e = list[j];                      // home | deferred chain << 30
         const int home = e & 0x3FFFFFFF, chain = (e >> 30) & 1;
         if (home >= a.d.n_homes) continue;
-        solve_direct<EXPLICIT, MODE>(a, home, smem, blockIdx.x, chain);
+        solve_direct<EXPLICIT, MODE, NW>(a, home, smem, blockIdx.x, chain);
         __syncthreads();
     }
 }
@@ -3180,7 +3463,7 @@ size_t workspace_bytes(const dragg_mpc_dims* d) {
     // deferred homes, [N][H+1][64] LP cost-to-go rows, the second launch's [SECOND_SLOTS][H][NF_BIG]
     // u16 back-pointers; round_lp: the back-pointers of its front DP
     if (d->int_mode == DRAGG_INT_ROUND_LP) return par_region_bytes(d->n_homes, d->horizon);
-    return direct_mode(d) ? big_region_offset(d->n_homes, d->horizon) + big_region_bytes(d->horizon) : 0;
+    return direct_mode(d) ? direct_workspace_bytes(d->n_homes, d->horizon) : 0;
 }
 
 // per home, the hot launch's (int_mode round: DM_FRONT)
@@ -3195,6 +3478,7 @@ int check_dims(const dragg_mpc_dims* d) {
     if (direct_mode(d) && !direct_fits(d->horizon)) return DRAGG_E_HORIZON;
     if (kernel_lds_bytes(d) > 160 * 1024) return DRAGG_E_HORIZON;
     if (direct_mode(d) && big_layout(d->horizon, d->sub_steps).bytes > 160 * 1024) return DRAGG_E_HORIZON;
+    if (direct_mode(d) && narrow_layout(d->horizon, d->sub_steps).bytes > 160 * 1024) return DRAGG_E_HORIZON;
     return DRAGG_OK;
 }
 
@@ -3252,16 +3536,25 @@ int launch(const KArgs& a, hipStream_t s) {
     if (!direct_mode(&a.d)) return launch_kernel(mpc_home_kernel<EXPLICIT>, attr[0], a, N, 64, kernel_lds_bytes(&a.d), s);
     if (N == 0) return DRAGG_OK;
     // the deferred list starts empty (its length word), then the hot launch, then the second
-    int* const len = reinterpret_cast<int*>(reinterpret_cast<char*>(a.p.workspace) + defer_offset(N, a.d.horizon)) + N;
+    char* const wsb = reinterpret_cast<char*>(a.p.workspace);
+    int* const len = reinterpret_cast<int*>(wsb + defer_offset(N, a.d.horizon)) + N;
+    int* const nlen = reinterpret_cast<int*>(wsb + narrow_list_offset(N, a.d.horizon)) + N;
     if (hipMemsetAsync(len, 0, sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
+    if (hipMemsetAsync(nlen, 0, sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
     const size_t lds = kernel_lds_bytes(&a.d);
     const int nw = hot_waves<EXPLICIT>(N, dev, lds);
-    const int rc = nw == 4 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 4>, attr[4], a, N, 4 * WAVE, lds, s)
-                 : nw == 2 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>, attr[3], a, N, 2 * WAVE, lds, s)
-                           : launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 1>, attr[1], a, N, WAVE, lds, s);
+    const char* fs = getenv("DRAGG_FORCE_STEP_DP");
+    KArgs b = a;
+    b.force_steps = (fs && fs[0] == '1') ? 1 : 0;
+    const int rc = nw == 4 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 4>, attr[4], b, N, 4 * WAVE, lds, s)
+                 : nw == 2 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>, attr[3], b, N, 2 * WAVE, lds, s)
+                           : launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 1>, attr[1], b, N, WAVE, lds, s);
     if (rc) return rc;
-    return launch_kernel(mpc_direct_kernel<EXPLICIT, DM_BUCKET>, attr[2], a, min(N, SECOND_SLOTS), WAVE,
-                         (size_t)big_layout(a.d.horizon, a.d.sub_steps).bytes, s);
+    const int rc2 = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_BUCKET>, attr[2], b, min(N, SECOND_SLOTS), WAVE,
+                                  (size_t)big_layout(a.d.horizon, a.d.sub_steps).bytes, s);
+    if (rc2) return rc2;
+    return launch_kernel(mpc_direct_kernel<EXPLICIT, DM_NARROW, NT_STEPS / WAVE>, attr[5], b, min(N, NARROW_SLOTS),
+                         NT_STEPS, (size_t)narrow_layout(a.d.horizon, a.d.sub_steps).bytes, s);
 }
 
 }  // namespace

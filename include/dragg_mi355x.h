@@ -169,11 +169,14 @@ typedef struct dragg_mpc_out {
                                    prices, 2 a feasible set narrower than one duty step,
                                    3 front overflow, 4 the exact pass's bound contradicts
                                    the bucketed schedule, 5 the exact DP was not run
-                                   (S != 6); bit 12 = solved by the second launch
-                                   (its front outgrew the hot launch's capacity; still
-                                   exact when bits 0-11 are 0); bits 13 / 14 = status
-                                   ROUND_FAIL decided by the indoor-air / tank chain
-                                   (no integer duty schedule for it)                     */
+                                   (S != 6), 6 the exact step-function DP past its
+                                   capacity; bit 12 = solved by a later launch (its front
+                                   outgrew the hot launch's capacity; still exact when
+                                   bits 0-11 are 0); bits 13 / 14 = status ROUND_FAIL
+                                   decided by the indoor-air / tank chain (no integer duty
+                                   schedule for it); bit 15 = solved by the exact
+                                   step-function DP (a feasible set narrower than one duty
+                                   step, mixed-sign prices, S != 6, a front past 2,048)  */
 } dragg_mpc_out;
 
 /* solver phases timed into dragg_mpc_out.cycles (diagnostic; NULL = not stamped) */

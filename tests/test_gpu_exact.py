@@ -156,3 +156,41 @@ def test_wide_band_rl_price_second_launch_exact(gpu):
         assert abs(obj[i] - opt) <= 1e-6 * max(1.0, abs(opt)), (i, obj[i], opt)
     print(f"wide band + RL price: {n_opt} of {len(homes)} homes optimal, all equal to the exact optimum")
     assert n_opt >= len(homes) // 2
+
+
+@pytest.mark.parametrize("name", F.scenarios())
+def test_step_function_dp_is_exact_on_every_record(name, gpu):
+    """The exact step-function DP (DM_NARROW: backward piecewise-constant value functions, no
+    dominance or sign assumption -- the launch that takes narrow feasible sets, mixed-sign prices
+    and S != 6) forced on EVERY record of every fixture (DRAGG_FORCE_STEP_DP=1): its thermal cost
+    equals the exact optimum to 1e-9 and the status agrees, mixed-sign RL prices included."""
+    import os
+    from dragg_amd import _lib as L
+    from oracle import mpc as M
+    d = F.load(name)
+    ex = _exact()[name]
+    os.environ["DRAGG_FORCE_STEP_DP"] = "1"
+    try:
+        res = _solve(d, "round")
+    finally:
+        os.environ.pop("DRAGG_FORCE_STEP_DP", None)
+    homes = {h["name"]: h for h in d["homes"]}
+    n = 0
+    for i, r in enumerate(d["records"]):
+        e = ex[i]
+        st = res["status"][i]
+        if st not in (L.ST_OPTIMAL, L.ST_ROUND_FAIL):
+            continue
+        has = e["cost_W"] is not None
+        assert (st == L.ST_OPTIMAL) == has, (name, i, L.STATUS_NAMES[st], e)
+        assert res["path"][i] == 0, (name, i, res["path"][i])          # no approximation
+        if not has:
+            continue
+        hc = M.home_const(homes[r["name"]])
+        u, wh, w = _thermal_cost(r, res["fc"], i, res["S"])
+        P = hc.Ph if r["season"] == "winter" else hc.Pc
+        ours = float(w @ (u * (hc.S * P)) + w @ (wh * (hc.S * hc.Pw)))
+        ref = e["cost_T"] + e["cost_W"]
+        assert abs(ours - ref) <= 1e-9 * max(1.0, abs(ref)), (name, i, ours, ref)
+        n += 1
+    print(f"{name}: {n} records solved by the step-function DP, all at the exact optimum")

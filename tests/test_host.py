@@ -154,11 +154,15 @@ def test_size_queries_without_gpu(lib_path):
     # u16 back-pointer per front label and stage (NB_CAP = 336), rounded to 256 B, then the
     # [N][8H] f64 stage-slot solutions and the [N] i32 list (+ its length) of the homes deferred to
     # the second launch, then (256-aligned) the front DP's LP cost-to-go rows [N][H + 1][64] (x, v),
-    # then (256-aligned) the second launch's back-pointer rows [512 blocks][H][NF_BIG = 2048] u16
+    # then (256-aligned) the second launch's back-pointer rows [512 blocks][H][NF_BIG = 2048] u16,
+    # then (256-aligned) the [N] i32 list (+ length) of homes for the step-function DP launch and
+    # (256-aligned) its storage: 8 blocks x ([2][H + 1][16384] + [2][16][16385]) f64
     par = (100 * 24 * 336 * 2 + 255) // 256 * 256
     w_off = (par + 100 * 8 * 24 * 8 + 101 * 4 + 255) // 256 * 256
     big_off = (w_off + 100 * 25 * 64 * 16 + 255) // 256 * 256
-    assert ws == big_off + 512 * 24 * 2048 * 2
+    nl_off = (big_off + 512 * 24 * 2048 * 2 + 255) // 256 * 256
+    nr_off = (nl_off + 101 * 4 + 255) // 256 * 256
+    assert ws == nr_off + 8 * (2 * 25 * 16384 + 2 * 16 * 16385) * 8
     lds_direct = lib.dragg_mpc_lds_bytes(ctypes.byref(d))
     assert 0 < lds_direct <= 13 * 1024                 # the hot launch: >= 12 homes per CU at H = 24
     d.horizon = 48
@@ -167,7 +171,7 @@ def test_size_queries_without_gpu(lib_path):
     d.int_mode = L.INT_RELAX
     assert lib.dragg_mpc_workspace_bytes(ctypes.byref(d)) == 0
     assert lib.dragg_mpc_lds_bytes(ctypes.byref(d)) > lds_direct
-    d.int_mode = 7
+    d.int_mode = 9
     assert lib.dragg_mpc_workspace_bytes(ctypes.byref(d)) < 0
     d.int_mode = L.INT_ROUND
     d.horizon = 400                                    # LP kernel's LDS is the binding limit

@@ -43,7 +43,7 @@ def run(tag, n, hours, dt, steps, month, seed_h, seed_w, seed, completable, out)
         agg.run_iteration()
         st = b.status.cpu().numpy()
         path = b.int_path.cpu().numpy()
-        narrow = np.array([reason(p, 0) == 2 or reason(p, 1) == 2 for p in path])
+        narrow = np.array([reason(p, 0) == 2 or reason(p, 1) == 2 or (int(p) & L.PATH_STEPS) != 0 for p in path])
         pick = np.flatnonzero((st == L.ST_ROUND_FAIL) | narrow)
         if len(pick) == 0:
             continue
