@@ -46,6 +46,9 @@ constexpr int NTB_BIG = 256;          // ... of the big exact pass (fronts up to
 constexpr int NT_STEPS = 1024;           // threads of a DM_NARROW block
 constexpr int STEP_CAP = 16384;          // breakpoints per value function
 constexpr int NARROW_SLOTS = 8;          // blocks of the persistent DM_NARROW launch
+constexpr int NF_MID = 384;              // front capacity of the mid launch (DM_MID)
+constexpr int NTB_MID = 128;             // ... and its key / cost buckets per stage
+constexpr int MID_SLOTS_MAX = 2048;      // blocks of the persistent mid launch (~7 per CU at H = 48)
 // exchange area of a multi-wave front DP: per-pass survivor masks, per-wave counts / ranges / minima
 constexpr int XCH_PASSES = 32;
 constexpr int XCH_BYTES = XCH_PASSES * 8 + 8 * 8 + 8 * 5 * 4;
@@ -1457,8 +1460,16 @@ __host__ __device__ inline size_t narrow_list_offset(int N, int H) {
 __host__ __device__ inline size_t narrow_region_offset(int N, int H) {
     return (narrow_list_offset(N, H) + (size_t)(N + 1) * sizeof(int) + 255) / 256 * 256;
 }
+// then the list of homes the mid launch hands to the big one ([N] i32 + length) and (256-aligned)
+// the mid launch's back-pointer rows [MID_SLOTS_MAX][H][NF_MID] u16
+__host__ __device__ inline size_t mid_list_offset(int N, int H) {
+    return (narrow_region_offset(N, H) + (size_t)NARROW_SLOTS * step_slot_bytes(H) + 255) / 256 * 256;
+}
+__host__ __device__ inline size_t mid_region_offset(int N, int H) {
+    return (mid_list_offset(N, H) + (size_t)(N + 1) * sizeof(int) + 255) / 256 * 256;
+}
 __host__ __device__ inline size_t direct_workspace_bytes(int N, int H) {
-    return narrow_region_offset(N, H) + (size_t)NARROW_SLOTS * step_slot_bytes(H);
+    return mid_region_offset(N, H) + (size_t)MID_SLOTS_MAX * H * NF_MID * sizeof(uint16_t);
 }
 
 struct DirectLayout {
@@ -1585,6 +1596,26 @@ __host__ __device__ inline BigLayout big_layout(int H, int S) {
     o.cb = take(8 * NTB_BIG, 16);
     o.mh = take(4 * NTB_BIG, 4);
     o.kl = take(4 * NTB_BIG, 4);
+    o.flo = take(4 * (H + 1), 4);
+    o.fhi = take(4 * (H + 1), 4);
+    o.bytes = (max(p, d.bytes) + 15) / 16 * 16;
+    return o;
+}
+
+// The mid launch: the direct layout, and over its DP arrays the exact pass's fronts [NF_MID],
+// W table, bucket arrays and hull: ~20 KB at H = 48, ~7 blocks per CU (the big layout: 2)
+__host__ __device__ inline BigLayout mid_layout(int H, int S) {
+    const DirectLayout d = direct_layout(H, S);
+    BigLayout o{};
+    int p = d.lab;
+    auto take = [&](int bytes, int align) { p = (p + align - 1) / align * align; const int r = p; p += bytes; return r; };
+    o.fa = take(16 * NF_MID, 16);
+    o.fb = take(16 * NF_MID, 16);
+    o.wl = take(8 * 3 * WAVE, 16);
+    o.kb = take(8 * NTB_MID, 16);
+    o.cb = take(8 * NTB_MID, 16);
+    o.mh = take(4 * NTB_MID, 4);
+    o.kl = take(4 * NTB_MID, 4);
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
     o.bytes = (max(p, d.bytes) + 15) / 16 * 16;
@@ -3166,18 +3197,20 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
 // labels (its own back-pointer rows per block), which replaces that schedule by the optimum.  Only
 // a chain that outgrows even NF_BIG keeps the bucketed schedule (int_path records it).  Keeping the
 // bucketed DP and the big pass out of DM_FRONT keeps their registers and LDS out of the hot kernel.
-enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1, DM_NARROW = 2 };
+enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1, DM_NARROW = 2, DM_MID = 3 };
 
 template <bool EXPLICIT, int MODE, int NW = 1>
 DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int first_chain) {
-    static_assert(NW == 1 || MODE != DM_BUCKET, "one wave per home in the second launch");
+    static_assert(NW == 1 || MODE == DM_FRONT || MODE == DM_NARROW, "one wave per home in the mid / big launches");
+    constexpr bool SECOND = MODE == DM_BUCKET || MODE == DM_MID;   // the bucketed DP + an exact big-front pass
     constexpr int NT = NW * WAVE;
     const int lane = threadIdx.x;
     const int N = a.d.n_homes;
     const int H = a.d.horizon;
     char* const ws = reinterpret_cast<char*>(a.p.workspace);
     int* const list = reinterpret_cast<int*>(ws + defer_offset(N, H));     // [N] + length at [N]
-    int* const nlist = reinterpret_cast<int*>(ws + narrow_list_offset(N, H));   // DM_BUCKET -> DM_NARROW
+    int* const nlist = reinterpret_cast<int*>(ws + narrow_list_offset(N, H));   // DM_MID / DM_BUCKET -> DM_NARROW
+    int* const blist = reinterpret_cast<int*>(ws + mid_list_offset(N, H));      // DM_MID -> DM_BUCKET
     Home h;
     LdsD D = MODE == DM_FRONT ? carve_front(smem, H) : carve_direct(smem, H, a.d.sub_steps);
     D.par = reinterpret_cast<uint16_t*>(ws) + (size_t)home * H * NB_CAP;
@@ -3293,7 +3326,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 if (!ok) int_path |= 1 << (13 + chain);
                 continue;
             }
-            if (h.S == 6 && !(MODE == DM_BUCKET && rl_prices)) {
+            if (h.S == 6 && !(SECOND && rl_prices)) {
                 double* const wl = D.wl;
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
                                    wg, wl, wl + WAVE, wl + 2 * WAVE, MODE == DM_FRONT ? D.xch : nullptr};
@@ -3336,10 +3369,12 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                         for (int k = lane; k < H; k += NT) c += D.cq[k] * D.x[k * 8 + sv];
                         ub = dpp_sum(c);
                     }
-                    const BigLayout bl = big_layout(H, a.d.sub_steps);
+                    const BigLayout bl = MODE == DM_MID ? mid_layout(H, a.d.sub_steps) : big_layout(H, a.d.sub_steps);
                     char* const sb = reinterpret_cast<char*>(smem);
                     double* const wl = reinterpret_cast<double*>(sb + bl.wl);
-                    uint16_t* const bpar = reinterpret_cast<uint16_t*>(ws + big_region_offset(N, H)) + (size_t)slot * H * NF_BIG;
+                    uint16_t* const bpar = MODE == DM_MID
+                        ? reinterpret_cast<uint16_t*>(ws + mid_region_offset(N, H)) + (size_t)slot * H * NF_MID
+                        : reinterpret_cast<uint16_t*>(ws + big_region_offset(N, H)) + (size_t)slot * H * NF_BIG;
                     const FrontBufs FB{reinterpret_cast<double2*>(sb + bl.fa), reinterpret_cast<double2*>(sb + bl.fb),
                                        reinterpret_cast<unsigned long long*>(sb + bl.kb),
                                        reinterpret_cast<unsigned long long*>(sb + bl.cb),
@@ -3348,7 +3383,14 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                                        D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE};
                     __syncthreads();
                     // keeps the bucketed schedule in D.x unless it finds (and writes) the optimum
-                    r2 = dp_front<6, NF_BIG, NF_BIG, NF_BIG, NTB_BIG>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
+                    if constexpr (MODE == DM_MID)
+                        r2 = dp_front<6, NF_MID, NF_MID, NF_MID, NTB_MID>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
+                    else
+                        r2 = dp_front<6, NF_BIG, NF_BIG, NF_BIG, NTB_BIG>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
+                    if (MODE == DM_MID && r2 == -3) {         // past NF_MID: the big launch's 2,048-label fronts
+                        if (lane == 0) blist[atomicAdd(blist + N, 1)] = home | (chain << 30);
+                        return;
+                    }
                     if (r2 == 1) ok = true;
                     else if (r2 == 0 && !ok) ok = false;      // exact: no integer schedule
                     else if (r2 == 0) r2 = -4;                // bound inconsistent with the schedule: keep it
@@ -3398,7 +3440,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
 }
 
 template <bool EXPLICIT, int MODE, int NW = 1>
-__global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_BUCKET ? 2 : 1) void mpc_direct_kernel(KArgs a) {
+__global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW ? 1 : 2) void mpc_direct_kernel(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     if (MODE == DM_FRONT) {
         if ((int)blockIdx.x < a.d.n_homes) solve_direct<EXPLICIT, MODE, NW>(a, blockIdx.x, smem, 0, 0);
@@ -3406,9 +3448,10 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_BUCKET
     }
     // persistent: block b solves the listed homes b, b + gridDim.x, ... (its own scratch rows in
     // the workspace: slot b); every block reaches the end of the list and exits
-    const int* const list = reinterpret_cast<const int*>(reinterpret_cast<const char*>(a.p.workspace) +
-                                                         (MODE == DM_BUCKET ? defer_offset(a.d.n_homes, a.d.horizon)
-                                                                            : narrow_list_offset(a.d.n_homes, a.d.horizon)));
+    const size_t lo = MODE == DM_MID ? defer_offset(a.d.n_homes, a.d.horizon)
+                    : MODE == DM_BUCKET ? mid_list_offset(a.d.n_homes, a.d.horizon)
+                                        : narrow_list_offset(a.d.n_homes, a.d.horizon);
+    const int* const list = reinterpret_cast<const int*>(reinterpret_cast<const char*>(a.p.workspace) + lo);
     const int cnt = min(list[a.d.n_homes], a.d.n_homes);
     for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
         const int e = list[j];                      // home | deferred chain << 30
@@ -3526,9 +3569,26 @@ int hot_waves(int N, int dev, size_t lds) {
     return N <= cap_dev[dev][2] ? 4 : N <= cap_dev[dev][1] ? 2 : 1;
 }
 
+// blocks of the persistent mid launch: as many as the GPU holds at once at its LDS (<= MID_SLOTS_MAX)
+template <bool EXPLICIT>
+int mid_slots(int dev, int H, int S) {
+    static int slots_dev[MAX_DEV] = {};
+    if (!slots_dev[dev]) {
+        hipDeviceProp_t prop{};
+        int per_cu = 0;
+        const void* k = (const void*)mpc_direct_kernel<EXPLICIT, DM_MID>;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+            hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, WAVE, (size_t)mid_layout(H, S).bytes) != hipSuccess)
+            return SECOND_SLOTS;
+        slots_dev[dev] = max(1, min(MID_SLOTS_MAX, per_cu * prop.multiProcessorCount));
+    }
+    return slots_dev[dev];
+}
+
 template <bool EXPLICIT>
 int launch(const KArgs& a, hipStream_t s) {
-    static int attr_dev[MAX_DEV][6] = {};
+    static int attr_dev[MAX_DEV][8] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return DRAGG_E_HIP;
     int* const attr = attr_dev[dev];
@@ -3539,8 +3599,10 @@ int launch(const KArgs& a, hipStream_t s) {
     char* const wsb = reinterpret_cast<char*>(a.p.workspace);
     int* const len = reinterpret_cast<int*>(wsb + defer_offset(N, a.d.horizon)) + N;
     int* const nlen = reinterpret_cast<int*>(wsb + narrow_list_offset(N, a.d.horizon)) + N;
+    int* const blen = reinterpret_cast<int*>(wsb + mid_list_offset(N, a.d.horizon)) + N;
     if (hipMemsetAsync(len, 0, sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
     if (hipMemsetAsync(nlen, 0, sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
+    if (hipMemsetAsync(blen, 0, sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
     const size_t lds = kernel_lds_bytes(&a.d);
     const int nw = hot_waves<EXPLICIT>(N, dev, lds);
     const char* fs = getenv("DRAGG_FORCE_STEP_DP");
@@ -3550,6 +3612,12 @@ int launch(const KArgs& a, hipStream_t s) {
                  : nw == 2 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>, attr[3], b, N, 2 * WAVE, lds, s)
                            : launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 1>, attr[1], b, N, WAVE, lds, s);
     if (rc) return rc;
+    // the deferred homes: the mid launch (fronts of 384 labels, many blocks), its overflows to the
+    // big launch (2,048 labels, 2 blocks per CU), what no front DP can take to the step-function DP
+    const int rcm = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_MID>, attr[6], b,
+                                  min(N, mid_slots<EXPLICIT>(dev, a.d.horizon, a.d.sub_steps)), WAVE,
+                                  (size_t)mid_layout(a.d.horizon, a.d.sub_steps).bytes, s);
+    if (rcm) return rcm;
     const int rc2 = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_BUCKET>, attr[2], b, min(N, SECOND_SLOTS), WAVE,
                                   (size_t)big_layout(a.d.horizon, a.d.sub_steps).bytes, s);
     if (rc2) return rc2;

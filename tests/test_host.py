@@ -162,7 +162,11 @@ def test_size_queries_without_gpu(lib_path):
     big_off = (w_off + 100 * 25 * 64 * 16 + 255) // 256 * 256
     nl_off = (big_off + 512 * 24 * 2048 * 2 + 255) // 256 * 256
     nr_off = (nl_off + 101 * 4 + 255) // 256 * 256
-    assert ws == nr_off + 8 * (2 * 25 * 16384 + 2 * 16 * 16385) * 8
+    # then (256-aligned) the [N] i32 list (+ length) the mid launch hands to the big one and
+    # (256-aligned) the mid launch's back-pointer rows [2048 blocks][H][NF_MID = 384] u16
+    ml_off = (nr_off + 8 * (2 * 25 * 16384 + 2 * 16 * 16385) * 8 + 255) // 256 * 256
+    mr_off = (ml_off + 101 * 4 + 255) // 256 * 256
+    assert ws == mr_off + 2048 * 24 * 384 * 2
     lds_direct = lib.dragg_mpc_lds_bytes(ctypes.byref(d))
     assert 0 < lds_direct <= 13 * 1024                 # the hot launch: >= 12 homes per CU at H = 24
     d.horizon = 48

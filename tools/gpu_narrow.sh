@@ -14,10 +14,12 @@ timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --cpu-seconds 0 > $OUT/
 for nw in 1 2 4; do
   DRAGG_WAVES_PER_HOME=$nw timeout -k 10 300 python3 bench.py --steps 96 --warmup 0 --cpu-seconds 0 --shard-of 8 > $OUT/shard8_nw$nw.json 2> $OUT/shard8_nw$nw.err || { echo "shard8 nw$nw failed"; exit 1; }
 done
+timeout -k 10 300 python3 bench.py --workload rl --steps 6 --warmup 1 --cpu-seconds 0 > $OUT/rl_smooth.json 2> $OUT/rl_smooth.err || { echo "rl failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_rl -o trace -- python3 bench.py --workload rl --steps 6 --warmup 1 --cpu-seconds 0 > $OUT/prof_rl.log 2>&1 || { echo "rl trace failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof96 -o trace -- python3 bench.py --steps 96 --warmup 0 --cpu-seconds 0 > $OUT/prof96.log 2>&1 || { echo "trace failed"; exit 1; }
 python3 - <<'PY'
 import json
-for f in ["full96", "driver20", "shard8_nw1", "shard8_nw2", "shard8_nw4"]:
+for f in ["full96", "driver20", "shard8_nw1", "shard8_nw2", "shard8_nw4", "rl_smooth"]:
     d = json.load(open(f"gpurun_out/r03b/{f}.json"))
     print(f, round(d["value"] / 1e6, 3), "M/s", round(d["ms_per_step"], 4), "ms/step", d["status_counts"])
 PY

@@ -15,6 +15,7 @@ steps + the committed step).  Per step (per action for RL):
 bench.py uses the file only when its key names the same workload and timed window."""
 import argparse
 import csv
+import re
 import json
 import os
 import sys
@@ -24,7 +25,8 @@ sys.path.insert(0, ROOT)
 
 
 def _hot(name):
-    return "mpc_direct_kernel<false, 0>" in name or "mpc_home_kernel<false>" in name
+    """the hot launch (any waves-per-home instance) or the LP kernel"""
+    return re.search(r"mpc_direct_kernel<false, 0[,>]", name) is not None or "mpc_home_kernel<false>" in name
 
 
 def step_groups(rows, n_units, per_unit, kernel_sub="mpc_"):
