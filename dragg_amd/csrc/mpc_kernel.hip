@@ -2541,7 +2541,17 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         if (H >= 2) wnext = load_row(2);
     }
     __syncthreads();
+#ifdef DRAGG_STAGE_PROF
+    // diagnostic: shader-clock cycles per stage section (0 ranges, 1 pass 1, 2 scans, 3 pass 3,
+    // 4 reductions / clears / W table, 5 stages), added into the S_PAD slots of stages 0..5
+    unsigned long long sp_acc[6] = {0, 0, 0, 0, 0, 0}, sp_t = __builtin_amdgcn_s_memtime();
+#define SP_MARK(i) do { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); sp_acc[i] += n_ - sp_t; sp_t = n_; } while (0)
+#endif
     for (int k = 0; k < H; ++k) {
+#ifdef DRAGG_STAGE_PROF
+        sp_acc[5] += 1;
+        sp_t = __builtin_amdgcn_s_memtime();
+#endif
         // a front past PRUNE_AT labels (a tariff boundary inside the horizon): build the LP
         // bound now and prune the remaining stages by it.  Only while the front fits the bounded
         // capacity (the W table's LDS follows it) -- and, when fa is that buffer, stays clear of it.
@@ -2590,6 +2600,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         // children are numbered c = NU * parent + duty and spread over the lanes (a stage
         // with n labels takes ceil(NU n / 64) passes, not NU ceil(n / 64))
         const int nc = n * NU;
+#ifdef DRAGG_STAGE_PROF
+        SP_MARK(0);
+#endif
         // 1. per key bucket the cheapest child (largest key among equally cheap ones), per
         //    cost bucket the largest-key child (cheapest among equal keys), both as
         //    understated bounds (cost up, key down), by 64-bit LDS atomics
@@ -2606,6 +2619,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             }
         }
         __syncthreads();
+#ifdef DRAGG_STAGE_PROF
+        SP_MARK(1);
+#endif
         // 2. mh[b] = min cost over the key buckets above b (lane l holds key chunk 63 - l:
         //    "above" = lower lanes, an exclusive prefix-min); kl[b] = max key over the cost
         //    buckets below b (lane l holds cost chunk l: an exclusive prefix-max)
@@ -2636,6 +2652,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             }
         }
         __syncthreads();
+#ifdef DRAGG_STAGE_PROF
+        SP_MARK(2);
+#endif
         // 3. survivors appended to the other buffer in (parent, duty) order.  A child X is
         //    dropped when one of four references provably dominates it (X's bounds
         //    overstated: key up, cost down):
@@ -2745,6 +2764,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
 #endif
         if (nn == 0) return 0;                       // no child left inside the feasible set
         if (nn > capn) return -3;                    // front overflow
+#ifdef DRAGG_STAGE_PROF
+        SP_MARK(3);
+#endif
         // the next stage's state and cost ranges from the survivors' positions: the exact
         // position V of a value lies in [v - 1, v + 2], widened past the back-conversion's
         // rounding
@@ -2766,9 +2788,15 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             if (k + 3 <= H) wnext = load_row(k + 3);
         }
         __syncthreads();
+#ifdef DRAGG_STAGE_PROF
+        SP_MARK(4);
+#endif
         double2* tmp = fa; fa = fb; fb = tmp;
         n = nn;
     }
+#ifdef DRAGG_STAGE_PROF
+    if (tid == 0) for (int i = 0; i < 6; ++i) B.x[i * 8 + S_PAD] += (double)sp_acc[i];
+#endif
     // the cheapest final label (lowest index on ties)
     double best = INFINITY;
     int bi = -1;

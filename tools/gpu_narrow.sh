@@ -23,4 +23,7 @@ for f in ["full96", "driver20", "shard8_nw1", "shard8_nw2", "shard8_nw4", "rl_sm
     d = json.load(open(f"gpurun_out/r03b/{f}.json"))
     print(f, round(d["value"] / 1e6, 3), "M/s", round(d["ms_per_step"], 4), "ms/step", d["status_counts"])
 PY
+DRAGG_LIB=varlib/sprof.so DRAGG_WAVES_PER_HOME=1 timeout -k 10 200 python3 tools/stage_prof.py --world 8 --steps 48 --out $OUT/stage_1250.json > /dev/null 2>&1 || { echo "stage prof failed"; exit 1; }
+DRAGG_LIB=varlib/sprof.so timeout -k 10 200 python3 tools/stage_prof.py --world 1 --steps 48 --out $OUT/stage_10k.json > /dev/null 2>&1 || { echo "stage prof 10k failed"; exit 1; }
+cat $OUT/stage_1250.json $OUT/stage_10k.json
 echo narrow-done
