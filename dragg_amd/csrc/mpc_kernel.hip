@@ -52,6 +52,8 @@ constexpr int MID_SLOTS_MAX = 2048;      // blocks of the persistent mid launch 
 // exchange area of a multi-wave front DP: per-pass survivor masks, per-wave counts / ranges / minima
 constexpr int XCH_PASSES = 32;
 constexpr int XCH_BYTES = XCH_PASSES * 8 + 8 * 8 + 8 * 5 * 4;
+constexpr int BM_HOT = 32;            // bound-mask passes of the hot launch (NF_HOT 7 / 64 = 19)
+constexpr int BM_MID = 48;            // ... of the mid launch (NF_MID 7 / 64 = 42)
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
 
 constexpr double SIGMA = 1e-6;
@@ -1415,6 +1417,7 @@ struct LdsD {
                                         //   battery LP runs after the thermal DPs)
     double* wl;                         // [3][WAVE] dp_front's W table (points, values, slopes)
     char* xch;                          // [XCH_BYTES] front_layout: a multi-wave DP's exchange area
+    unsigned long long* bm;             // [BM_HOT] front_layout: pass-1 bound masks
     uint16_t* par;                      // [H][NB_CAP] DP back-pointers (global workspace)
 };
 
@@ -1451,8 +1454,10 @@ __host__ __device__ inline size_t big_region_bytes(int H) { return (size_t)SECON
 // (256-aligned) DM_NARROW's step-function storage, one region per block of that launch
 __host__ __device__ inline size_t step_slot_bytes(int H) {
     // V_k breakpoints and values [H + 1][STEP_CAP] f64 each, merged candidates and interval values
-    // [(16)(STEP_CAP + 1)] f64 each (S <= 15)
-    return ((size_t)2 * (H + 1) * STEP_CAP + (size_t)2 * 16 * (STEP_CAP + 1)) * sizeof(double);
+    // [(16)(STEP_CAP + 1)] f64 each (S <= 15), then the merged candidates' origins [16 (STEP_CAP + 1)]
+    // i32 and the pairwise rank tables [16 x 15][STEP_CAP + 1] i32
+    return ((size_t)2 * (H + 1) * STEP_CAP + (size_t)2 * 16 * (STEP_CAP + 1)) * sizeof(double) +
+           (size_t)(16 + 16 * 15) * (STEP_CAP + 1) * sizeof(int);
 }
 __host__ __device__ inline size_t narrow_list_offset(int N, int H) {
     return (big_region_offset(N, H) + big_region_bytes(H) + 255) / 256 * 256;
@@ -1476,7 +1481,8 @@ struct DirectLayout {
     int draw, oat, ghi, price, cA, cC, cq, sc, t2, bx0, bp1, bp2, lab, rmin, tail;
     int kb, cb, mh, kl, flo, fhi;             // dp_front tail
     int cand, rt, candp, tarr, rsrc;          // dp_zspace tail
-    int wl, sgS, sgL, xch;                    // front_layout only: W table, battery segment lists, exchange
+    int wl, sgS, sgL, xch, bm;                // front_layout only: W table, battery segment lists, exchange,
+                                              //   bound masks
     int bytes;
 };
 
@@ -1507,6 +1513,7 @@ __host__ __device__ inline DirectLayout front_layout(int H) {
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
     o.xch = take(XCH_BYTES, 16);
+    o.bm = take(8 * BM_HOT, 8);
     const int dp_end = p;
     p = o.tail;                                  // the battery LP's arrays over the dead DP region
     o.sgS = take(16 * seg_cap(H), 16);
@@ -1565,7 +1572,7 @@ __host__ __device__ inline int direct_lds_bytes(int H, int S) { return direct_la
 
 // DM_NARROW: the direct layout, then the step DP's LDS: counts [H + 1] i32, scan scratch, the
 // reachable hull [2][H + 1] f64
-struct NarrowLayout { int cnt, red, rl, rh, bytes; };
+struct NarrowLayout { int cnt, red, rl, rh, bs, bytes; };
 __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
     NarrowLayout o{};
     int p = direct_layout(H, S).bytes;
@@ -1574,6 +1581,7 @@ __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
     o.red = take(4 * (NT_STEPS / 64 + 2), 4);
     o.rl = take(8 * (H + 1), 8);
     o.rh = take(8 * (H + 1), 8);
+    o.bs = take(8 * STEP_CAP, 16);
     o.bytes = (p + 15) / 16 * 16;
     return o;
 }
@@ -1582,7 +1590,7 @@ __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
 // is done with them, its schedule is in the global solution array) the big exact pass's
 // fronts [NF_BIG], W table, bucket arrays and hull.
 struct BigLayout {
-    int fa, fb, wl, kb, cb, mh, kl, flo, fhi, bytes;
+    int fa, fb, wl, kb, cb, mh, kl, flo, fhi, bm, bytes;
 };
 __host__ __device__ inline BigLayout big_layout(int H, int S) {
     const DirectLayout d = direct_layout(H, S);
@@ -1618,6 +1626,7 @@ __host__ __device__ inline BigLayout mid_layout(int H, int S) {
     o.kl = take(4 * NTB_MID, 4);
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
+    o.bm = take(8 * BM_MID, 8);
     o.bytes = (max(p, d.bytes) + 15) / 16 * 16;
     return o;
 }
@@ -1643,6 +1652,7 @@ DEV LdsD carve_front(double* smem, int H) {
     L.sgS = D(o.sgS); L.sgL = D(o.sgL);
     L.bx0 = D(o.bx0); L.bp1 = D(o.bp1); L.bp2 = D(o.bp2); L.t2 = D(o.t2);
     L.xch = b + o.xch;
+    L.bm = reinterpret_cast<unsigned long long*>(b + o.bm);
     L.par = nullptr;                                             // set by the kernel
     return L;
 }
@@ -2283,6 +2293,8 @@ struct FrontBufs {
                                          //   +inf padded; nullptr = no bound pruning
     double *wlx, *wlv, *wls;             // [WAVE] LDS: the current stage's W (points, slopes)
     char* xch;                           // [XCH_BYTES] LDS: the waves' exchange area (NW > 1)
+    unsigned long long* bmask;           // [bmask_cap] LDS: per pass of 64 children, which passed the
+    int bmask_cap;                       //   box and LP-bound tests in pass 1 (nullptr: recomputed)
 };
 
 // 1 / w to about 1 ulp: v_rcp_f64 and one Newton step (no IEEE division sequence)
@@ -2424,7 +2436,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         const int m = j < WAVE ? read_lane(wc0, j) : read_lane(wc1, j - WAVE);
         return lane < m ? B.wg[j * WAVE + lane] : make_double2(INFINITY, INFINITY);
     };
-    auto make_bound = [&]() -> bool {
+    // kf: the stage the DP continues from (rows W_{kf+1} .. W_H are built); the greedy upper bound
+    // starts there from a label (gx0, c0) of the front (a feasible completion of it bounds the optimum)
+    auto make_bound = [&](int kf, double gx0, double c0) -> bool {
         if (H >= 2 * WAVE) return false;                 // row counts held for 128 rows (a 32 h horizon)
         bool prune = true;
         {
@@ -2435,7 +2449,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             int m = 2;
             if (wid == 0 && lane < m) B.wg[H * WAVE + lane] = make_double2(wx, wv);
             set_count(H, m);
-            for (int j = H - 1; j >= 1; --j) {
+            for (int j = H - 1; j >= max(1, kf + 1); --j) {
                 const double A = B.cA[j], C = B.cC[j], q = B.cq[j];
                 if (!(A > 0.0) || m + 1 > WAVE) { prune = false; break; }
                 const double zs = g * SS, cS = q * SS;
@@ -2487,11 +2501,11 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             double qabs = 0.0;
             for (int k = lane; k < H; k += WAVE) qabs += fabs(B.cq[k]) * SS;
             qabs = dpp_sum(qabs);
-            double gx = x0, ub = 0.0;
+            double gx = gx0, ub = c0;
             bool gok = true;
             // (the W table is wave 0's to load and write; every wave reads it)
-            double2 cur = wid == 0 ? load_row(1) : make_double2(INFINITY, INFINITY);
-            for (int k = 0; k < H && gok; ++k) {
+            double2 cur = wid == 0 ? load_row(kf + 1) : make_double2(INFINITY, INFINITY);
+            for (int k = kf; k < H && gok; ++k) {
                 double2 nxt = (wid == 0 && k + 2 <= H) ? load_row(k + 2) : make_double2(INFINITY, INFINITY);
                 if (wid == 0) w_to_lds(B, lane, cur.x, cur.y);
                 __syncthreads();
@@ -2521,7 +2535,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         }
         return prune;
     };
-    bool prune = B.wg != nullptr && (use_bound || nodom) && make_bound();
+    bool prune = B.wg != nullptr && (use_bound || nodom) && make_bound(0, x0, 0.0);
     if (nodom && !prune) return nodom && (pos && neg) ? -1 : -2;
     int capn = prune ? CAPB : CAP;                   // front capacity (overflow: -3)
     bool tried = prune || B.wg == nullptr;           // the bound is built at most once
@@ -2557,7 +2571,32 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         // capacity (the W table's LDS follows it) -- and, when fa is that buffer, stays clear of it.
         if (!tried && n > PRUNE_AT && n <= CAPB) {
             tried = true;
-            if (make_bound()) {
+            // the rows from this stage on, the greedy bound from the front's cheapest label
+            double bc = INFINITY, bx = 0.0;
+            int bi = -1;
+            for (int i = tid; i < n; i += NT) {
+                const double2 Li = fa[i];
+                if (Li.y < bc) { bc = Li.y; bx = Li.x; bi = i; }
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                const double oc = __shfl_xor(bc, o), ox = __shfl_xor(bx, o);
+                const int oi = __shfl_xor(bi, o);
+                if (oc < bc || (oc == bc && oi >= 0 && (bi < 0 || oi < bi))) { bc = oc; bx = ox; bi = oi; }
+            }
+            if constexpr (NW > 1) {
+                __syncthreads();
+                if (lane == 0) { xbest[wid] = bc; xint[wid] = (unsigned)bi; }
+                __syncthreads();
+                bc = xbest[0]; bi = (int)xint[0];
+                for (int w = 1; w < NW; ++w) {
+                    const double oc = xbest[w];
+                    const int oi = (int)xint[w];
+                    if (oc < bc || (oc == bc && oi >= 0 && (bi < 0 || oi < bi))) { bc = oc; bi = oi; }
+                }
+                bx = fa[bi].x;
+                __syncthreads();
+            }
+            if (make_bound(k, bx, bc)) {
                 prune = true;
                 capn = CAPB;
                 if (wid == 0) {
@@ -2606,12 +2645,19 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         // 1. per key bucket the cheapest child (largest key among equally cheap ones), per
         //    cost bucket the largest-key child (cheapest among equal keys), both as
         //    understated bounds (cost up, key down), by 64-bit LDS atomics
+        // (with the bound on, pass 3 reuses pass 1's box + bound decisions: one W lookup per child)
+        const bool cache = prune && !nodom && B.bmask != nullptr && (nc + WAVE - 1) / WAVE <= B.bmask_cap;
         for (int c = tid; c < nc && !nodom; c += NT) {
             const int i = c / NU, u = c - i * NU;
             const double2 Li = fa[i];
             const double xc = fma(A, Li.x, fma(g, (double)u, C));
             const double cc = fma(q, (double)u, Li.y);
-            if (xc >= bl && xc <= bh && (!prune || cc + w_eval(B, xc) <= UBT)) {
+            const bool in = xc >= bl && xc <= bh && (!prune || cc + w_eval(B, xc) <= UBT);
+            if (cache) {
+                const unsigned long long bal = __ballot(in);
+                if (lane == 0) B.bmask[c / WAVE] = bal;
+            }
+            if (in) {
                 const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
                 const unsigned cu = vc + 2u, kd = dn(vk);
                 atomicMin(&B.kb[min(NBK - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
@@ -2675,8 +2721,13 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             cc = fma(q, (double)u, Li.y);
             vk = fixp(fma(xc, kmul, kadd));
             vc = fixp(fma(cc, csc, cadd));
-            bool keep = have && xc >= bl && xc <= bh;
-            if (keep && prune) keep = cc + w_eval(B, xc) <= UBT;
+            bool keep;
+            if (cache) {
+                keep = have && ((B.bmask[c / WAVE] >> (c & (WAVE - 1))) & 1ull);
+            } else {
+                keep = have && xc >= bl && xc <= bh;
+                if (keep && prune) keep = cc + w_eval(B, xc) <= UBT;
+            }
             if (keep && !nodom) {
                 const int kbk = min(NBK - 1, (int)(vk >> 23)), cbk = min(NBK - 1, (int)(vc >> 23));
                 const unsigned ku = vk + 2u, cd = dn(vc);
@@ -2856,6 +2907,7 @@ DEV bool round_duties(const Home& h, const Lds& L, int lane, uint16_t* par) {
     B.cA = cA; B.cC = cC; B.cq = cq; B.x = L.x; B.par = par;
     B.wg = nullptr; B.wlx = B.wlv = B.wls = nullptr;     // no bound pruning on this path
     B.xch = nullptr;                                     // one wave
+    B.bmask = nullptr; B.bmask_cap = 0;                  // bound off here
     const bool front = h.S == 6 && par != nullptr && (f - L.Lf) <= 128 * H;
     for (int k = lane; k < H; k += WAVE) {
         cA[k] = h.aT;
@@ -3052,6 +3104,9 @@ struct StepBufs {
     int* red;                    // LDS [NT / 64 + 1] scan scratch
     double* rl;                  // LDS [H + 1] reachable hull of x_k (widened)
     double* rh;
+    int* corig;                  // [(S + 1)(STEP_CAP + 1)] origin (u np + i) of each merged point
+    int* rk;                     // [(S + 1) S][STEP_CAP + 1] ranks: points of list u2 before point i of list u
+    double* bs;                  // LDS [STEP_CAP]: the breakpoints of V_{k+1} while V_k is built
 };
 
 template <int NT>
@@ -3093,26 +3148,53 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         const double* V = VV + (size_t)(k + 1) * STEP_CAP;
         const int m = Sb.cnt[k + 1];                     // values; m + 1 breakpoints
         const int np = m + 1;
-        auto P = [&](int u, int i) { return (B[i] - C - g * (double)u) * iA; };     // preimage points
-        // number of points of list u below p (or <= p)
-        auto below = [&](int u, double p, bool le) {
+        double* const Bs = Sb.bs;
+        for (int i = tid; i < np; i += NT) Bs[i] = B[i];
+        __syncthreads();
+        // list u holds the preimages P_u(i) = (K_u(i) - C) / A of V_{k+1}'s breakpoints under duty u,
+        // with K_u(i) = B_i - g u.  The lists are merged by the keys K (one rounding each; P is a
+        // monotone function of K, so the merged P are sorted, equal neighbours giving zero-width
+        // intervals), ties broken by lower duty.
+        auto key = [&](int u, int i) { return Bs[i] - g * (double)u; };
+        // (1a) pairwise ranks rk[u][u2][i] = points of list u2 before point i of list u: two pointers
+        //      over contiguous chunks of i (one binary search per chunk, then a monotone walk)
+        constexpr int CH = 32;
+        const int nch = (np + CH - 1) / CH;
+        const int npair = NU * (NU - 1);
+        for (int w = tid; w < npair * nch; w += NT) {
+            const int pr = w / nch, ch = w - pr * nch;
+            const int u = pr / (NU - 1), u2r = pr - u * (NU - 1), u2 = u2r + (u2r >= u ? 1 : 0);
+            const bool le = u2 < u;                       // lower duty first on equal keys
+            const int i0 = ch * CH, i1 = min(np, i0 + CH);
+            const double k0 = key(u, i0);
             int a = 0, b = np;
             while (a < b) {
                 const int c = (a + b) >> 1;
-                const double v = P(u, c);
-                if (le ? v <= p : v < p) a = c + 1; else b = c;
+                const double v = key(u2, c);
+                if (le ? v <= k0 : v < k0) a = c + 1; else b = c;
             }
-            return a;
+            int* const row = Sb.rk + (size_t)pr * (STEP_CAP + 1);
+            for (int i = i0; i < i1; ++i) {
+                const double ki = key(u, i);
+                while (a < np && (le ? key(u2, a) <= ki : key(u2, a) < ki)) ++a;
+                row[i] = a;
+            }
+        }
+        __syncthreads();
+        auto rank_in = [&](int u, int i, int u2) -> int {   // points of list u2 before point (u, i)
+            if (u2 == u) return i;
+            const int pr = u * (NU - 1) + (u2 < u ? u2 : u2 - 1);
+            return Sb.rk[(size_t)pr * (STEP_CAP + 1) + i];
         };
-        // (1) merge the NU lists by rank (ties: lower duty first, then lower index)
+        // (1b) every candidate to its merged position
         const int Mc = NU * np;
         for (int idx = tid; idx < Mc; idx += NT) {
             const int u = idx / np, i = idx - u * np;
-            const double p = P(u, i);
             int r = i;
             for (int u2 = 0; u2 < NU; ++u2)
-                if (u2 != u) r += below(u2, p, u2 < u);
-            Sb.cand[r] = p;
+                if (u2 != u) r += rank_in(u, i, u2);
+            Sb.cand[r] = (key(u, i) - C) * iA;
+            Sb.corig[r] = idx;
         }
         __syncthreads();
         // (2) elementary intervals of the domain D_k = box of x_k and reachable hull
@@ -3128,16 +3210,19 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             jh = a;
         }
         const int T = jh - jl + 1;                        // intervals [e_t, e_{t+1})
-        // (3) each interval's value at its midpoint; NaN marks a zero-width interval
+        // (3) each interval's value: V_{k+1} of list u's interval holding the interval (the points
+        //     of list u up to merged position jl + t - 1), min over u; NaN marks zero width
         for (int t = tid; t < T; t += NT) {
             const double e0 = t == 0 ? dl : Sb.cand[jl + t - 1];
             const double e1 = t == T - 1 ? dh : Sb.cand[jl + t];
             double best = NAN;
             if (e1 > e0) {
-                const double mid = 0.5 * (e0 + e1);
                 best = INFINITY;
+                const int pos = jl + t - 1;               // the last merged point at or below e0
+                const int o = pos >= 0 ? Sb.corig[pos] : 0;
+                const int uo = o / np, io = o - uo * np;
                 for (int u = 0; u < NU; ++u) {
-                    const int i = below(u, mid, true) - 1;       // interval of list u holding mid
+                    const int i = pos < 0 ? -1 : (u == uo ? io : rank_in(uo, io, u) - 1);
                     if (i >= 0 && i < m) best = fmin(best, fma(q, (double)u, V[i]));
                 }
             }
@@ -3339,10 +3424,13 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 const NarrowLayout nl = narrow_layout(H, a.d.sub_steps);
                 char* const sb = reinterpret_cast<char*>(smem);
                 double* const sw = reinterpret_cast<double*>(ws + narrow_region_offset(N, H) + (size_t)slot * step_slot_bytes(H));
+                double* const sw2 = sw + (size_t)2 * (H + 1) * STEP_CAP + (size_t)32 * (STEP_CAP + 1);
                 const StepBufs SB{sw, sw + (size_t)(H + 1) * STEP_CAP, sw + (size_t)2 * (H + 1) * STEP_CAP,
                                   sw + (size_t)2 * (H + 1) * STEP_CAP + (size_t)16 * (STEP_CAP + 1),
                                   reinterpret_cast<int*>(sb + nl.cnt), reinterpret_cast<int*>(sb + nl.red),
-                                  reinterpret_cast<double*>(sb + nl.rl), reinterpret_cast<double*>(sb + nl.rh)};
+                                  reinterpret_cast<double*>(sb + nl.rl), reinterpret_cast<double*>(sb + nl.rh),
+                                  reinterpret_cast<int*>(sw2), reinterpret_cast<int*>(sw2) + (size_t)16 * (STEP_CAP + 1),
+                                  reinterpret_cast<double*>(sb + nl.bs)};
                 r = dp_steps<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, D.x, sx, sv, lane);
                 if (r >= 0) {
                     ok = r == 1;
@@ -3357,7 +3445,8 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
             if (h.S == 6 && !(SECOND && rl_prices)) {
                 double* const wl = D.wl;
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
-                                   wg, wl, wl + WAVE, wl + 2 * WAVE, MODE == DM_FRONT ? D.xch : nullptr};
+                                   wg, wl, wl + WAVE, wl + 2 * WAVE, MODE == DM_FRONT ? D.xch : nullptr,
+                                   MODE == DM_FRONT ? D.bm : nullptr, MODE == DM_FRONT ? BM_HOT : 0};
                 if constexpr (MODE == DM_FRONT)
                     r = dp_front<6, NF_HOT, NF_HOT, NB_CAP, NTB_HOT, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
                 else
@@ -3408,7 +3497,9 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                                        reinterpret_cast<unsigned long long*>(sb + bl.cb),
                                        reinterpret_cast<unsigned*>(sb + bl.mh), reinterpret_cast<unsigned*>(sb + bl.kl),
                                        reinterpret_cast<unsigned*>(sb + bl.flo), reinterpret_cast<unsigned*>(sb + bl.fhi),
-                                       D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE};
+                                       D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE, nullptr,
+                                       MODE == DM_MID ? reinterpret_cast<unsigned long long*>(sb + bl.bm) : nullptr,
+                                       MODE == DM_MID ? BM_MID : 0};
                     __syncthreads();
                     // keeps the bucketed schedule in D.x unless it finds (and writes) the optimum
                     if constexpr (MODE == DM_MID)

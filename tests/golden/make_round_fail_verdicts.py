@@ -18,7 +18,7 @@ rows, `mpc_calc.py:291-446`, T and Tw coupled through e T_{k+1}) is given to HiG
 Verdicts whose HiGHS run hit the time limit are recorded as undecided (None).
 Output: tests/golden/proven/round_fail_joint.json.gz (inputs + verdicts).
 
-Usage: python tests/golden/make_round_fail_verdicts.py CASES.json [workers] [time_limit]"""
+Usage: python tests/golden/make_round_fail_verdicts.py CASES.json [workers] [rf_time_limit] [narrow_time_limit]"""
 import gzip
 import json
 import multiprocessing as mp
@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 
 def decide(args):
-    case, limit = args
+    case, limits = args
     from scipy.optimize import milp, LinearConstraint, Bounds
     from oracle import mpc as M
     from oracle import thermal as TH
@@ -45,6 +45,7 @@ def decide(args):
     P = M.build_problem(hc, si)
     cons = [LinearConstraint(P["A_eq"], P["b_eq"], P["b_eq"]), LinearConstraint(P["A_ub"], -np.inf, P["b_ub"])]
     rf = case["status"] == "round_fail"
+    limit = limits[0] if rf else limits[1]
     c = np.zeros_like(P["c"]) if rf else P["c"]
     t0 = time.time()
     res = milp(c, constraints=cons, integrality=P["integrality"], bounds=Bounds(-np.inf, np.inf),
@@ -79,17 +80,22 @@ def main():
     cases = json.load(open(sys.argv[1]))
     workers = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     limit = float(sys.argv[3]) if len(sys.argv) > 3 else 1800.0
+    nlimit = float(sys.argv[4]) if len(sys.argv) > 4 else limit
+    # every verdict is also appended to a journal as it arrives (a long run can be cut short)
+    journal = open(os.path.join(HERE, "proven", "round_fail_joint.partial.jsonl"), "a")
     with mp.get_context("fork").Pool(workers) as pool:
         res = []
-        for r in pool.imap_unordered(decide, [(c, limit) for c in cases]):
+        for r in pool.imap_unordered(decide, [(c, (limit, nlimit)) for c in cases]):
             res.append(r)
+            journal.write(json.dumps(r) + "\n")
+            journal.flush()
             print(f"{r['source']} t={r['t']} i={r['i']} {r['status']}: joint feasible {r['joint_feasible']} "
                   f"(HiGHS {r['highs_status']}, {r['highs_seconds']:.1f}s), sequential {r['sequential_feasible']}",
                   flush=True)
     res.sort(key=lambda r: (r["source"], r["t"], r["i"]))
     path = os.path.join(HERE, "proven", "round_fail_joint.json.gz")
     with gzip.open(path, "wt") as f:
-        json.dump({"cases": res, "time_limit": limit,
+        json.dump({"cases": res, "time_limit": limit, "narrow_time_limit": nlimit,
                    "note": "HiGHS on the reference's full model: round_fail = feasibility (zero objective), "
                            "narrow = proven optimum; joint_feasible None = undecided within the limit"}, f)
     n_rf = [r for r in res if r["status"] == "round_fail"]
