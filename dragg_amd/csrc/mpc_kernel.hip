@@ -52,8 +52,6 @@ constexpr int MID_SLOTS_MAX = 2048;      // blocks of the persistent mid launch 
 // exchange area of a multi-wave front DP: per-pass survivor masks, per-wave counts / ranges / minima
 constexpr int XCH_PASSES = 32;
 constexpr int XCH_BYTES = XCH_PASSES * 8 + 8 * 8 + 8 * 5 * 4;
-constexpr int BM_HOT = 32;            // bound-mask passes of the hot launch (NF_HOT 7 / 64 = 19)
-constexpr int BM_MID = 48;            // ... of the mid launch (NF_MID 7 / 64 = 42)
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
 
 constexpr double SIGMA = 1e-6;
@@ -1195,6 +1193,7 @@ struct KArgs {
     const double* noise;
     int t;
     int force_steps;       // diagnostic (DRAGG_FORCE_STEP_DP=1): every home to the exact step DP
+    int no_steps;          // diagnostic (DRAGG_NO_STEP_DP=1): keep the bucketed schedule instead (round 2)
 };
 
 // --------------------------------------------------------------------------------------
@@ -1417,7 +1416,6 @@ struct LdsD {
                                         //   battery LP runs after the thermal DPs)
     double* wl;                         // [3][WAVE] dp_front's W table (points, values, slopes)
     char* xch;                          // [XCH_BYTES] front_layout: a multi-wave DP's exchange area
-    unsigned long long* bm;             // [BM_HOT] front_layout: pass-1 bound masks
     uint16_t* par;                      // [H][NB_CAP] DP back-pointers (global workspace)
 };
 
@@ -1481,8 +1479,7 @@ struct DirectLayout {
     int draw, oat, ghi, price, cA, cC, cq, sc, t2, bx0, bp1, bp2, lab, rmin, tail;
     int kb, cb, mh, kl, flo, fhi;             // dp_front tail
     int cand, rt, candp, tarr, rsrc;          // dp_zspace tail
-    int wl, sgS, sgL, xch, bm;                // front_layout only: W table, battery segment lists, exchange,
-                                              //   bound masks
+    int wl, sgS, sgL, xch;                    // front_layout only: W table, battery segment lists, exchange
     int bytes;
 };
 
@@ -1513,7 +1510,6 @@ __host__ __device__ inline DirectLayout front_layout(int H) {
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
     o.xch = take(XCH_BYTES, 16);
-    o.bm = take(8 * BM_HOT, 8);
     const int dp_end = p;
     p = o.tail;                                  // the battery LP's arrays over the dead DP region
     o.sgS = take(16 * seg_cap(H), 16);
@@ -1590,7 +1586,7 @@ __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
 // is done with them, its schedule is in the global solution array) the big exact pass's
 // fronts [NF_BIG], W table, bucket arrays and hull.
 struct BigLayout {
-    int fa, fb, wl, kb, cb, mh, kl, flo, fhi, bm, bytes;
+    int fa, fb, wl, kb, cb, mh, kl, flo, fhi, bytes;
 };
 __host__ __device__ inline BigLayout big_layout(int H, int S) {
     const DirectLayout d = direct_layout(H, S);
@@ -1626,7 +1622,6 @@ __host__ __device__ inline BigLayout mid_layout(int H, int S) {
     o.kl = take(4 * NTB_MID, 4);
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
-    o.bm = take(8 * BM_MID, 8);
     o.bytes = (max(p, d.bytes) + 15) / 16 * 16;
     return o;
 }
@@ -1652,7 +1647,6 @@ DEV LdsD carve_front(double* smem, int H) {
     L.sgS = D(o.sgS); L.sgL = D(o.sgL);
     L.bx0 = D(o.bx0); L.bp1 = D(o.bp1); L.bp2 = D(o.bp2); L.t2 = D(o.t2);
     L.xch = b + o.xch;
-    L.bm = reinterpret_cast<unsigned long long*>(b + o.bm);
     L.par = nullptr;                                             // set by the kernel
     return L;
 }
@@ -2293,8 +2287,6 @@ struct FrontBufs {
                                          //   +inf padded; nullptr = no bound pruning
     double *wlx, *wlv, *wls;             // [WAVE] LDS: the current stage's W (points, slopes)
     char* xch;                           // [XCH_BYTES] LDS: the waves' exchange area (NW > 1)
-    unsigned long long* bmask;           // [bmask_cap] LDS: per pass of 64 children, which passed the
-    int bmask_cap;                       //   box and LP-bound tests in pass 1 (nullptr: recomputed)
 };
 
 // 1 / w to about 1 ulp: v_rcp_f64 and one Newton step (no IEEE division sequence)
@@ -2645,19 +2637,12 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         // 1. per key bucket the cheapest child (largest key among equally cheap ones), per
         //    cost bucket the largest-key child (cheapest among equal keys), both as
         //    understated bounds (cost up, key down), by 64-bit LDS atomics
-        // (with the bound on, pass 3 reuses pass 1's box + bound decisions: one W lookup per child)
-        const bool cache = prune && !nodom && B.bmask != nullptr && (nc + WAVE - 1) / WAVE <= B.bmask_cap;
         for (int c = tid; c < nc && !nodom; c += NT) {
             const int i = c / NU, u = c - i * NU;
             const double2 Li = fa[i];
             const double xc = fma(A, Li.x, fma(g, (double)u, C));
             const double cc = fma(q, (double)u, Li.y);
-            const bool in = xc >= bl && xc <= bh && (!prune || cc + w_eval(B, xc) <= UBT);
-            if (cache) {
-                const unsigned long long bal = __ballot(in);
-                if (lane == 0) B.bmask[c / WAVE] = bal;
-            }
-            if (in) {
+            if (xc >= bl && xc <= bh && (!prune || cc + w_eval(B, xc) <= UBT)) {
                 const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
                 const unsigned cu = vc + 2u, kd = dn(vk);
                 atomicMin(&B.kb[min(NBK - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
@@ -2721,13 +2706,8 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             cc = fma(q, (double)u, Li.y);
             vk = fixp(fma(xc, kmul, kadd));
             vc = fixp(fma(cc, csc, cadd));
-            bool keep;
-            if (cache) {
-                keep = have && ((B.bmask[c / WAVE] >> (c & (WAVE - 1))) & 1ull);
-            } else {
-                keep = have && xc >= bl && xc <= bh;
-                if (keep && prune) keep = cc + w_eval(B, xc) <= UBT;
-            }
+            bool keep = have && xc >= bl && xc <= bh;
+            if (keep && prune) keep = cc + w_eval(B, xc) <= UBT;
             if (keep && !nodom) {
                 const int kbk = min(NBK - 1, (int)(vk >> 23)), cbk = min(NBK - 1, (int)(vc >> 23));
                 const unsigned ku = vk + 2u, cd = dn(vc);
@@ -2907,7 +2887,6 @@ DEV bool round_duties(const Home& h, const Lds& L, int lane, uint16_t* par) {
     B.cA = cA; B.cC = cC; B.cq = cq; B.x = L.x; B.par = par;
     B.wg = nullptr; B.wlx = B.wlv = B.wls = nullptr;     // no bound pruning on this path
     B.xch = nullptr;                                     // one wave
-    B.bmask = nullptr; B.bmask_cap = 0;                  // bound off here
     const bool front = h.S == 6 && par != nullptr && (f - L.Lf) <= 128 * H;
     for (int k = lane; k < H; k += WAVE) {
         cA[k] = h.aT;
@@ -3141,6 +3120,11 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
     }
     __syncthreads();
     const int NU = S + 1;
+#ifdef DRAGG_STEP_PROF
+    unsigned long long spa[6] = {0, 0, 0, 0, 0, 0}, spt = __builtin_amdgcn_s_memtime();
+    long long sp_np = 0, sp_max = 0;
+#define STP(i) do { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); spa[i] += n_ - spt; spt = n_; } while (0)
+#endif
     for (int k = H - 1; k >= 1; --k) {
         const double A = cA[k], C = cC[k], q = cq[k];
         const double iA = 1.0 / A;
@@ -3186,6 +3170,9 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             const int pr = u * (NU - 1) + (u2 < u ? u2 : u2 - 1);
             return Sb.rk[(size_t)pr * (STEP_CAP + 1) + i];
         };
+#ifdef DRAGG_STEP_PROF
+        STP(0);
+#endif
         // (1b) every candidate to its merged position
         const int Mc = NU * np;
         for (int idx = tid; idx < Mc; idx += NT) {
@@ -3197,6 +3184,9 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             Sb.corig[r] = idx;
         }
         __syncthreads();
+#ifdef DRAGG_STEP_PROF
+        STP(1);
+#endif
         // (2) elementary intervals of the domain D_k = box of x_k and reachable hull
         const double dl = fmax(boxlo(k - 1), Sb.rl[k]), dh = fmin(boxhi(k - 1), Sb.rh[k]);
         if (!(dl <= dh)) return 0;
@@ -3229,6 +3219,9 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             Sb.ival[t] = best;
         }
         __syncthreads();
+#ifdef DRAGG_STEP_PROF
+        STP(2);
+#endif
         // (4) compaction: drop zero-width intervals, then merge equal neighbours (two block scans
         //     over contiguous per-thread chunks, so that order is kept)
         const int per = (T + NT - 1) / NT;
@@ -3264,7 +3257,14 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             if (j == 0 || kv[j] != kv[j - 1]) { OB[o2] = ks[j]; OV[o2] = kv[j]; ++o2; }
         if (tid == 0) { OB[tot2] = dh; Sb.cnt[k] = tot2; }
         __syncthreads();
+#ifdef DRAGG_STEP_PROF
+        STP(3);
+        sp_np += np; sp_max = max(sp_max, (long long)np);
+#endif
     }
+#ifdef DRAGG_STEP_PROF
+    STP(4);
+#endif
     // forward recovery (wave 0: duty u on lane u): the cheapest q u + V_{k+1}(x') over the
     // duties whose successor stays in its box, lowest duty on ties (the oracle's rule)
     bool ok = true;
@@ -3297,6 +3297,10 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         if (lane == 0) Sb.cnt[0] = ok ? 1 : 0;
     }
     __syncthreads();
+#ifdef DRAGG_STEP_PROF
+    STP(5);
+    if (tid == 0) { for (int i = 0; i < 6; ++i) X[(10 + i) * 8 + S_PAD] += (double)spa[i]; X[16 * 8 + S_PAD] += (double)sp_np; X[17 * 8 + S_PAD] = fmax(X[17 * 8 + S_PAD], (double)sp_max); }
+#endif
     return Sb.cnt[0];
 }
 
@@ -3445,8 +3449,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
             if (h.S == 6 && !(SECOND && rl_prices)) {
                 double* const wl = D.wl;
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
-                                   wg, wl, wl + WAVE, wl + 2 * WAVE, MODE == DM_FRONT ? D.xch : nullptr,
-                                   MODE == DM_FRONT ? D.bm : nullptr, MODE == DM_FRONT ? BM_HOT : 0};
+                                   wg, wl, wl + WAVE, wl + 2 * WAVE, MODE == DM_FRONT ? D.xch : nullptr};
                 if constexpr (MODE == DM_FRONT)
                     r = dp_front<6, NF_HOT, NF_HOT, NB_CAP, NTB_HOT, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
                 else
@@ -3467,7 +3470,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
             } else if (MODE == DM_FRONT) {                 // leave the home to DM_BUCKET
                 if (lane == 0) list[atomicAdd(list + N, 1)] = home | (chain << 30);
                 return;
-            } else if (r == -1 || r == -2 || (r == -5 && !rl_prices)) {
+            } else if (!a.no_steps && (r == -1 || r == -2 || (r == -5 && !rl_prices))) {
                 // no dominance here (mixed-sign prices without a usable bound, a feasible set
                 // narrower than one duty step, S != 6): the exact step-function DP of DM_NARROW
                 if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30);
@@ -3497,9 +3500,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                                        reinterpret_cast<unsigned long long*>(sb + bl.cb),
                                        reinterpret_cast<unsigned*>(sb + bl.mh), reinterpret_cast<unsigned*>(sb + bl.kl),
                                        reinterpret_cast<unsigned*>(sb + bl.flo), reinterpret_cast<unsigned*>(sb + bl.fhi),
-                                       D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE, nullptr,
-                                       MODE == DM_MID ? reinterpret_cast<unsigned long long*>(sb + bl.bm) : nullptr,
-                                       MODE == DM_MID ? BM_MID : 0};
+                                       D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE};
                     __syncthreads();
                     // keeps the bucketed schedule in D.x unless it finds (and writes) the optimum
                     if constexpr (MODE == DM_MID)
@@ -3513,7 +3514,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                     if (r2 == 1) ok = true;
                     else if (r2 == 0 && !ok) ok = false;      // exact: no integer schedule
                     else if (r2 == 0) r2 = -4;                // bound inconsistent with the schedule: keep it
-                    if (r2 < 0) {                             // past NF_BIG: the exact step-function DP
+                    if (r2 < 0 && !a.no_steps) {              // past NF_BIG: the exact step-function DP
                         if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30);
                         return;
                     }
@@ -3727,6 +3728,8 @@ int launch(const KArgs& a, hipStream_t s) {
     const char* fs = getenv("DRAGG_FORCE_STEP_DP");
     KArgs b = a;
     b.force_steps = (fs && fs[0] == '1') ? 1 : 0;
+    const char* ns = getenv("DRAGG_NO_STEP_DP");
+    b.no_steps = (ns && ns[0] == '1') ? 1 : 0;
     const int rc = nw == 4 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 4>, attr[4], b, N, 4 * WAVE, lds, s)
                  : nw == 2 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>, attr[3], b, N, 2 * WAVE, lds, s)
                            : launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 1>, attr[1], b, N, WAVE, lds, s);
