@@ -43,7 +43,7 @@ constexpr int NTB_HOT = 64;           // key / cost buckets per stage of the hot
                                       //   (small fronts: a one-bucket-per-lane scan; measured 128: +6 % time)
 constexpr int NTB = 192;              // ... of the second launch's regular front DP and round_lp
 constexpr int NTB_BIG = 256;          // ... of the big exact pass (fronts up to NF_BIG)
-constexpr int NT_STEPS = 1024;           // threads of a DM_NARROW block
+constexpr int NT_STEPS = 512;            // threads of a DM_NARROW block (8 waves: 256 VGPRs, no spills)
 constexpr int STEP_CAP = 16384;          // breakpoints per value function
 constexpr int NARROW_SLOTS = 8;          // blocks of the persistent DM_NARROW launch
 constexpr int NF_MID = 384;              // front capacity of the mid launch (DM_MID)
