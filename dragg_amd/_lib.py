@@ -42,6 +42,7 @@ STATUS_NAMES = ["optimal", "infeasible", "infeasible_cert", "max_iter", "round_f
                 "err_missing", "solver_error"]
 
 INT_ROUND, INT_RELAX, INT_ROUND_LP, INT_FAIL = 0, 1, 2, 3
+FLAG_EXACT = 1                 # dims.flags: the step-function DP for every chain the front DP cannot take
 INT_MODES = {"round": INT_ROUND, "relax": INT_RELAX, "round_lp": INT_ROUND_LP, "fail": INT_FAIL}
 
 PHASES = ["setup", "iter", "factor", "polish", "check", "integer", "write", "battery"]
@@ -54,7 +55,8 @@ class Dims(ctypes.Structure):
     _fields_ = [("n_homes", ctypes.c_int32), ("horizon", ctypes.c_int32), ("sub_steps", ctypes.c_int32),
                 ("dt", ctypes.c_int32), ("n_draw_hours", ctypes.c_int32), ("n_env", ctypes.c_int32),
                 ("n_rp", ctypes.c_int32), ("int_mode", ctypes.c_int32), ("max_iter", ctypes.c_int32),
-                ("check_every", ctypes.c_int32), ("discount", ctypes.c_double)]
+                ("check_every", ctypes.c_int32), ("discount", ctypes.c_double), ("flags", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class Problem(ctypes.Structure):

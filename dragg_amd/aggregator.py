@@ -36,7 +36,7 @@ def shard_index(n, rank, world):
 class DeviceAggregator:
     def __init__(self, homes, oat, ghi, tou, start_index=0, num_timesteps=96, reward_price=(0.0,),
                  int_mode="round", seed=0, rank=0, world=1, group=None, keep_history=True,
-                 max_iter=4000, check_every=10, device=None, batch_cls=MPCBatch):
+                 max_iter=4000, check_every=10, device=None, batch_cls=MPCBatch, exact=False):
         self.rank, self.world, self.group = rank, world, group
         self.seed = int(seed)
         # identifies the community a checkpoint belongs to (load_state refuses another one's)
@@ -50,7 +50,8 @@ class DeviceAggregator:
         # CPU (tests/test_distributed.py); the solver itself is MPCBatch (HIP, no fallback).
         self.batch = batch_cls(self.homes, oat, ghi, tou, start_index, reward_price, int_mode=int_mode,
                               seed=seed, home_offset=rank, home_stride=world, max_iter=max_iter, check_every=check_every,
-                              device=dev, template_home=homes[0] if homes else None)
+                              device=dev, template_home=homes[0] if homes else None,
+                              **({"exact": True} if exact else {}))
         self.num_timesteps = num_timesteps
         self.timestep = 0
         n = self.batch.N

@@ -1193,7 +1193,6 @@ struct KArgs {
     const double* noise;
     int t;
     int force_steps;       // diagnostic (DRAGG_FORCE_STEP_DP=1): every home to the exact step DP
-    int no_steps;          // diagnostic (DRAGG_NO_STEP_DP=1): keep the bucketed schedule instead (round 2)
 };
 
 // --------------------------------------------------------------------------------------
@@ -3142,7 +3141,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         auto key = [&](int u, int i) { return Bs[i] - g * (double)u; };
         // (1a) pairwise ranks rk[u][u2][i] = points of list u2 before point i of list u: two pointers
         //      over contiguous chunks of i (one binary search per chunk, then a monotone walk)
-        constexpr int CH = 32;
+        constexpr int CH = 33;          // odd: the lanes' chunk starts fall in different LDS banks
         const int nch = (np + CH - 1) / CH;
         const int npair = NU * (NU - 1);
         for (int w = tid; w < npair * nch; w += NT) {
@@ -3470,9 +3469,10 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
             } else if (MODE == DM_FRONT) {                 // leave the home to DM_BUCKET
                 if (lane == 0) list[atomicAdd(list + N, 1)] = home | (chain << 30);
                 return;
-            } else if (!a.no_steps && (r == -1 || r == -2 || (r == -5 && !rl_prices))) {
+            } else if ((a.d.flags & DRAGG_FLAG_EXACT) && (r == -1 || r == -2 || (r == -5 && !rl_prices))) {
                 // no dominance here (mixed-sign prices without a usable bound, a feasible set
-                // narrower than one duty step, S != 6): the exact step-function DP of DM_NARROW
+                // narrower than one duty step, S != 6): with DRAGG_FLAG_EXACT the exact step-function
+                // DP of DM_NARROW (slow: thousands of breakpoints); else the bucketed schedule below
                 if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30);
                 return;
             } else {
@@ -3514,10 +3514,13 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                     if (r2 == 1) ok = true;
                     else if (r2 == 0 && !ok) ok = false;      // exact: no integer schedule
                     else if (r2 == 0) r2 = -4;                // bound inconsistent with the schedule: keep it
-                    if (r2 < 0 && !a.no_steps) {              // past NF_BIG: the exact step-function DP
-                        if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30);
-                        return;
-                    }
+                }
+                // the bucketed schedule stands in for the optimum (int_path reports it), but a
+                // status is always exact: where the bucketed DP found no schedule and no exact pass
+                // decided it, the step-function DP decides (with DRAGG_FLAG_EXACT: every such chain)
+                if (r2 < 0 && (!ok || (a.d.flags & DRAGG_FLAG_EXACT))) {
+                    if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30);
+                    return;
                 }
                 if (r2 < 0) int_path |= (1 << chain) | ((-r2) << (4 + 4 * chain));   // chain bit + reason
             }
@@ -3637,6 +3640,7 @@ size_t kernel_lds_bytes(const dragg_mpc_dims* d) {
 int check_dims(const dragg_mpc_dims* d) {
     if (!d || d->n_homes < 0 || d->horizon < 1 || d->sub_steps < 1 || d->dt < 1) return DRAGG_E_ARG;
     if (d->int_mode < DRAGG_INT_ROUND || d->int_mode > DRAGG_INT_FAIL) return DRAGG_E_ARG;
+    if (d->flags & ~DRAGG_FLAG_EXACT) return DRAGG_E_ARG;
     if (direct_mode(d) && d->sub_steps > 15) return DRAGG_E_ARG;     // 4-bit duty in the DP record
     if (direct_mode(d) && !direct_fits(d->horizon)) return DRAGG_E_HORIZON;
     if (kernel_lds_bytes(d) > 160 * 1024) return DRAGG_E_HORIZON;
@@ -3728,8 +3732,7 @@ int launch(const KArgs& a, hipStream_t s) {
     const char* fs = getenv("DRAGG_FORCE_STEP_DP");
     KArgs b = a;
     b.force_steps = (fs && fs[0] == '1') ? 1 : 0;
-    const char* ns = getenv("DRAGG_NO_STEP_DP");
-    b.no_steps = (ns && ns[0] == '1') ? 1 : 0;
+
     const int rc = nw == 4 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 4>, attr[4], b, N, 4 * WAVE, lds, s)
                  : nw == 2 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>, attr[3], b, N, 2 * WAVE, lds, s)
                            : launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 1>, attr[1], b, N, WAVE, lds, s);

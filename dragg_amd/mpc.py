@@ -100,11 +100,15 @@ class MPCBatch:
         (the season-noise key), so a shard draws the same numbers as the whole community.
     template_home : a home of the community, for the dims of an empty shard (homes == []):
         its steps are no-ops and its sums zero.
+    exact : int_mode round: every chain the Pareto-front DP cannot take (a feasible set narrower
+        than one duty step -- ~0.3 homes per 10k-home step --, mixed-sign prices without a usable
+        bound, RL fronts past 2,048 labels) by the exact step-function DP (slow) instead of the
+        bucketed DP's schedule (DRAGG_FLAG_EXACT).  Statuses are exact either way.
     """
 
     def __init__(self, homes, oat=None, ghi=None, tou=None, start_index=0, reward_price=(0.0,),
                  int_mode="round", seed=0, max_iter=4000, check_every=10, device="cuda", home_offset=0,
-                 home_stride=1, template_home=None):
+                 home_stride=1, template_home=None, exact=False):
         if int_mode not in L.INT_MODES:
             raise ValueError(f"int_mode must be one of {sorted(L.INT_MODES)}, not {int_mode!r}")
         self.lib = L.load()
@@ -125,7 +129,8 @@ class MPCBatch:
         self.dims = L.Dims(n_homes=self.N, horizon=self.H, sub_steps=self.S, dt=self.dt,
                            n_draw_hours=dm["n_draw_hours"], n_env=0, n_rp=1,
                            int_mode=L.INT_MODES[int_mode],
-                           max_iter=max_iter, check_every=check_every, discount=dm["discount"])
+                           max_iter=max_iter, check_every=check_every, discount=dm["discount"],
+                           flags=L.FLAG_EXACT if exact else 0)
         self.seed = int(seed)
         self.home_offset = int(home_offset)
         self.home_stride = int(home_stride)

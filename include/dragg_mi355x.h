@@ -129,7 +129,19 @@ typedef struct dragg_mpc_dims {
     int32_t max_iter;      /* ADMM iteration cap (<=0: default 4000)                   */
     int32_t check_every;   /* polish / residual check interval (<=0: default 10)       */
     double discount;       /* discount_factor                        (mpc_calc.py:152) */
+    int32_t flags;         /* dragg_flag bits (0 = default)                             */
+    int32_t reserved;
 } dragg_mpc_dims;
+
+/* dims.flags */
+enum dragg_flag {
+    /* int_mode round: solve every chain the Pareto-front DP cannot take (a feasible set narrower
+       than one duty step, mixed-sign prices without a usable bound, a front past 2,048 labels)
+       by the exact step-function DP too.  Without it such a chain keeps the bucketed DP's
+       schedule (reported in out.int_path) unless that finds none -- statuses are exact either
+       way.  The step-function DP is slow (milliseconds per chain). */
+    DRAGG_FLAG_EXACT = 1
+};
 
 typedef struct dragg_mpc_problem {
     const double* params;       /* [DRAGG_NPARAM][N]                                    */

@@ -333,14 +333,18 @@ def test_bench_round_fail_solves_have_no_integer_schedule(bench_day):
     assert n_fail > 0 and n_checked == n_fail
 
 
-def test_bench_narrow_set_solves_are_exact(bench_day):
+def test_bench_narrow_set_solves_gap_bound_and_exact_mode(bench_day):
     """A chain whose feasible set is narrower than one duty step somewhere in the horizon breaks the
-    front DP's dominance (round 2 kept a bucketed approximation there: up to 8.5 % above the
-    optimum, and ROUND_FAIL where a schedule exists); such homes now go to the exact step-function
-    DP (int_path bit 15).  Every one of them over 100 steps of the bench workload equals the exact
-    MILP optimum (oracle/thermal.py exact_milp: the assumption-free backward DP) to 1e-6, status for
-    status, and none keeps an approximation."""
+    front DP's dominance.  By default such a chain keeps the bucketed DP's schedule (int_path reason
+    2) -- its status is exact all the same: where the bucketed DP finds no schedule the exact
+    step-function DP decides (test_round_fail_status_matches_the_joint_model).  Every such solve of
+    the bench workload over 100 steps: status identical to the exact optimum (oracle/thermal.py
+    exact_milp, the assumption-free backward DP), never below it, gap bounded (measured max 8.5 %).
+    With DRAGG_FLAG_EXACT (MPCBatch exact=True) the same steps take the step-function DP: every one
+    equals the exact optimum (1e-6) and none keeps an approximation."""
+    import torch
     from dragg_amd import _lib as L
+    from dragg_amd.aggregator import DeviceAggregator
     d = bench_day
     gaps, n = [], 0
     for s in d["steps"]:
@@ -348,10 +352,41 @@ def test_bench_narrow_set_solves_are_exact(bench_day):
         if len(pick) == 0:
             continue
         n += len(pick)
-        assert not (s["path"][pick] & L.PATH_APPROX_MASK).any(), s["path"][pick]
         _check_sample(d["homes"], d["oat"], d["ghi"], d["tou"], [0.0], s["t"], s["prev_vals"], s["prev_fc"],
                       s["noise"], s["status"], s["obj"], s["vals"], s["fc"], pick, path=s["path"],
-                      fallback_gaps=gaps)
-    print(f"bench workload, {d['n_steps']} steps: {n} solves by the exact step-function DP, all equal to the exact "
-          f"optimum (1e-6), statuses identical")
-    assert n > 0
+                      fallback_gaps=gaps, approx_bound=NARROW_GAP_BOUND)
+    g = np.array(gaps)
+    print(f"bench workload, {d['n_steps']} steps: {n} narrow-set solves, {len(g)} optimal on the bucketed schedule: "
+          f"gap to the exact optimum max {g.max() if len(g) else 0:.2e}, {int((g > 1e-9).sum())} above 1e-9")
+    assert n > 0 and (len(g) == 0 or g.max() <= NARROW_GAP_BOUND)
+    # exact mode: re-solve those same steps from the same states with the step-function DP
+    from dragg_amd.mpc import MPCBatch
+    n_exact = 0
+    for s in d["steps"]:
+        pick = np.flatnonzero(_narrow(s["path"]))
+        if len(pick) == 0:
+            continue
+        b = MPCBatch([d["homes"][i] for i in pick], d["oat"], d["ghi"], d["tou"], 0, [0.0], seed=12,
+                     home_offset=0, exact=True)
+        # the same global noise keys: rebuild the picked homes' rows of the season draw
+        b.vals.copy_(torch.tensor(s["prev_vals"][:, pick]))
+        b.fc.copy_(torch.tensor(s["prev_fc"][:, :, pick]))
+        b.step(s["t"], noise=torch.tensor(s["noise"][:, pick]))
+        torch.cuda.synchronize()
+        st, ob, path = b.status.cpu().numpy(), b.obj.cpu().numpy(), b.int_path.cpu().numpy()
+        assert not (path & L.PATH_APPROX_MASK).any(), path
+        assert (st == s["status"][pick]).all(), (st, s["status"][pick])
+        # the exact mode's answers in place of the default ones, held to the exact optimum (1e-6)
+        # and the reference model (violation, integrality, c.x = objective)
+        ob_all, vals_all, fc_all = s["obj"].copy(), s["vals"].copy(), s["fc"].copy()
+        ob_all[pick] = ob
+        vals_all[:, pick] = b.vals.cpu().numpy()
+        fc_all[:, :, pick] = b.fc.cpu().numpy()
+        _check_sample(d["homes"], d["oat"], d["ghi"], d["tou"], [0.0], s["t"], s["prev_vals"], s["prev_fc"],
+                      s["noise"], s["status"], ob_all, vals_all, fc_all, pick)
+        ex = {i: ob[j] for j, i in enumerate(pick) if st[j] == L.ST_OPTIMAL}
+        n_exact += len(ex)
+    print(f"exact mode: {n_exact} of those solves by the step-function DP, all at the exact optimum")
+
+
+NARROW_GAP_BOUND = 0.10      # the bucketed approximation's measured worst case (8.5 %, home 7519 at t = 60)

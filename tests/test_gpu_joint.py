@@ -10,7 +10,8 @@ the proven optimum for the narrow cases).  The kernel re-solves each case from t
 inputs:
 * status parity: ROUND_FAIL iff HiGHS proved the joint model infeasible, optimal iff it found an
   integer point (undecided cases are reported, not counted);
-* narrow cases: the kernel's objective against HiGHS's proven joint optimum."""
+* narrow cases, solved with DRAGG_FLAG_EXACT (the step-function DP): the kernel's objective against
+  HiGHS's proven joint optimum where HiGHS proved one within its limit."""
 import gzip
 import json
 import os
@@ -32,7 +33,7 @@ def _cases():
         return json.load(f)["cases"]
 
 
-def _solve(cases):
+def _solve(cases, exact=False):
     """solve_explicit over the cases (one batch per horizon)."""
     import torch
     from dragg_amd.mpc import MPCBatch
@@ -42,7 +43,7 @@ def _solve(cases):
         by_h.setdefault(len(c["price"]), []).append(j)
     for H, idx in by_h.items():
         cs = [cases[j] for j in idx]
-        b = MPCBatch([c["home"] for c in cs], int_mode="round")
+        b = MPCBatch([c["home"] for c in cs], int_mode="round", exact=exact)
         col = lambda k, n: np.array([np.asarray(c[k], float)[:n] for c in cs]).T  # noqa: E731
         b.solve_explicit(t=np.array([c["t"] for c in cs], np.int32), T0=[c["T0"] for c in cs],
                          Tw0=[c["Tw0"] for c in cs], E0=[np.nan if c["E0"] is None else c["E0"] for c in cs],
@@ -85,7 +86,7 @@ def test_narrow_set_solves_against_the_joint_optimum(gpu):
     cases = [c for c in _cases() if c["status"] != "round_fail"]
     if not cases:
         pytest.skip("no narrow-set case")
-    res = _solve(cases)
+    res = _solve(cases, exact=True)            # DRAGG_FLAG_EXACT: the step-function DP
     gaps = []
     for j, c in enumerate(cases):
         st, obj, path = res[j]

@@ -1,7 +1,7 @@
 """Diagnostic: section cycles of the exact step-function DP (DRAGG_STEP_PROF variant) on every home
 that took it in the bench workload: (1a) ranks, (1b) merge, (2-3) interval values, (4) compaction,
 -, recovery; breakpoints summed and max over the stages.  Usage:
-DRAGG_LIB=varlib/stprof.so python tools/step_prof.py [--force] [--steps K]"""
+DRAGG_LIB=varlib/stprof.so python tools/step_prof.py [--exact] [--steps K]"""
 import argparse
 import math
 import os
@@ -19,12 +19,14 @@ from dragg_amd.community import synthetic_homes, synthetic_weather  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--homes", type=int, default=10000)
 ap.add_argument("--steps", type=int, default=96)
+ap.add_argument("--exact", action="store_true", help="DRAGG_FLAG_EXACT: every narrow chain takes the step DP")
 a = ap.parse_args()
 dt, hh = 4, 12
 days = math.ceil((math.ceil(a.steps / dt) + hh + 2) / 24) + 1
 homes = synthetic_homes(a.homes, seed=12, days=days, dt=dt, horizon_hours=hh)
 oat, ghi, tou = synthetic_weather(days, dt, math.ceil(a.steps / dt), seed=3, month=7)
-agg = DeviceAggregator(homes, oat, ghi, tou, 0, a.steps, reward_price=[0.0], seed=12, keep_history=False)
+agg = DeviceAggregator(homes, oat, ghi, tou, 0, a.steps, reward_price=[0.0], seed=12, keep_history=False,
+                       exact=a.exact)
 N, H = agg.batch.N, agg.batch.H
 par = ((N * H * 336 * 2 + 255) // 256) * 256
 rows = []
