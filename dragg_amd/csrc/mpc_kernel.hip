@@ -50,8 +50,11 @@ constexpr int NF_MID = 384;              // front capacity of the mid launch (DM
 constexpr int NTB_MID = 128;             // ... and its key / cost buckets per stage
 constexpr int MID_SLOTS_MAX = 2048;      // blocks of the persistent mid launch (~7 per CU at H = 48)
 // exchange area of a multi-wave front DP: per-pass survivor masks, per-wave counts / ranges / minima
-constexpr int XCH_PASSES = 32;
-constexpr int XCH_BYTES = XCH_PASSES * 8 + 8 * 8 + 8 * 5 * 4;
+// (one mask per 64-child pass of a full front of `cap` labels with S = 6: 7 children per label)
+__host__ __device__ constexpr int xch_passes(int cap) { return (cap * 7 + 63) / 64; }
+__host__ __device__ constexpr int xch_bytes(int cap) { return xch_passes(cap) * 8 + 8 * 8 + 8 * 5 * 4; }
+constexpr int NW_MID = 1;                // waves per home of the mid launch
+constexpr int NW_BIG = 4;                // waves per home of the big launch (2 blocks per CU: 8 waves)
 enum Slot { S_U = 0, S_W = 1, S_T = 2, S_TW = 3, S_CH = 4, S_DIS = 5, S_E = 6, S_PAD = 7 };
 
 constexpr double SIGMA = 1e-6;
@@ -1414,7 +1417,7 @@ struct LdsD {
     double *sgS, *sgL;                  // battery segments [2][seg_cap], in lab / rmin (the
                                         //   battery LP runs after the thermal DPs)
     double* wl;                         // [3][WAVE] dp_front's W table (points, values, slopes)
-    char* xch;                          // [XCH_BYTES] front_layout: a multi-wave DP's exchange area
+    char* xch;                          // [xch_bytes(cap)] a multi-wave DP's exchange area
     uint16_t* par;                      // [H][NB_CAP] DP back-pointers (global workspace)
 };
 
@@ -1508,7 +1511,7 @@ __host__ __device__ inline DirectLayout front_layout(int H) {
     o.kl = take(4 * NTB_HOT, 4);
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
-    o.xch = take(XCH_BYTES, 16);
+    o.xch = take(xch_bytes(NF_HOT), 16);
     const int dp_end = p;
     p = o.tail;                                  // the battery LP's arrays over the dead DP region
     o.sgS = take(16 * seg_cap(H), 16);
@@ -1585,7 +1588,7 @@ __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
 // is done with them, its schedule is in the global solution array) the big exact pass's
 // fronts [NF_BIG], W table, bucket arrays and hull.
 struct BigLayout {
-    int fa, fb, wl, kb, cb, mh, kl, flo, fhi, bytes;
+    int fa, fb, wl, kb, cb, mh, kl, flo, fhi, xch, bytes;
 };
 __host__ __device__ inline BigLayout big_layout(int H, int S) {
     const DirectLayout d = direct_layout(H, S);
@@ -1601,7 +1604,9 @@ __host__ __device__ inline BigLayout big_layout(int H, int S) {
     o.kl = take(4 * NTB_BIG, 4);
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
-    o.bytes = (max(p, d.bytes) + 15) / 16 * 16;
+    p = max(p, d.bytes);                         // past the direct layout too: the regular front DP of
+    o.xch = take(max(xch_bytes(NF_BIG), xch_bytes(NF)), 16);   // the (multi-wave) launch uses it as well
+    o.bytes = (p + 15) / 16 * 16;
     return o;
 }
 
@@ -1621,7 +1626,9 @@ __host__ __device__ inline BigLayout mid_layout(int H, int S) {
     o.kl = take(4 * NTB_MID, 4);
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
-    o.bytes = (max(p, d.bytes) + 15) / 16 * 16;
+    p = max(p, d.bytes);
+    o.xch = take(max(xch_bytes(NF_MID), xch_bytes(NF)), 16);
+    o.bytes = (p + 15) / 16 * 16;
     return o;
 }
 
@@ -2285,7 +2292,7 @@ struct FrontBufs {
     double2* wg;                         // [H + 1][WAVE] global: LP cost-to-go W_j as points (x, v),
                                          //   +inf padded; nullptr = no bound pruning
     double *wlx, *wlv, *wls;             // [WAVE] LDS: the current stage's W (points, slopes)
-    char* xch;                           // [XCH_BYTES] LDS: the waves' exchange area (NW > 1)
+    char* xch;                           // [xch_bytes(CAP)] LDS: the waves' exchange area (NW > 1)
 };
 
 // 1 / w to about 1 ulp: v_rcp_f64 and one Newton step (no IEEE division sequence)
@@ -2349,10 +2356,11 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     constexpr int NT = NW * WAVE;
     const int lane = tid & (WAVE - 1);
     const int wid = NW > 1 ? tid / WAVE : 0;
-    static_assert(NW == 1 || CAP * (SS + 1) <= XCH_PASSES * WAVE, "the exchange area holds 32 passes");
+    constexpr int XP = xch_passes(CAP);
+    static_assert(NW == 1 || (SS == 6 && NW <= 8), "the exchange area is sized for S = 6 and up to 8 waves");
     unsigned long long* const xmask = reinterpret_cast<unsigned long long*>(B.xch);
-    double* const xbest = reinterpret_cast<double*>(B.xch + XCH_PASSES * 8);
-    unsigned* const xint = reinterpret_cast<unsigned*>(B.xch + XCH_PASSES * 8 + 8 * 8);   // [5][8]
+    double* const xbest = reinterpret_cast<double*>(B.xch + XP * 8);
+    unsigned* const xint = reinterpret_cast<unsigned*>(B.xch + XP * 8 + 8 * 8);   // [5][8]
     static_assert(SS > 0 && SS < 16, "duty count must be a compile-time constant below 16");
     static_assert(CAP <= PS && CAPB <= PS && PS <= 4096, "back-pointer rows hold a 12-bit parent index");
     constexpr int NU = SS + 1;
@@ -3089,7 +3097,12 @@ struct StepBufs {
 
 template <int NT>
 DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const double* cq, int H, int S, double g,
-                 double x0, double lo0, double hi0, double lo, double hi, double* X, int sx, int sv, int tid) {
+                 double x0, double lo0, double hi0, double lo, double hi, double* X, int sx, int sv, int tid,
+                 bool feas_only = false) {
+    // feas_only: every duty cost taken as 0, so V_k is 0 on the states with a feasible continuation and
+    // +inf elsewhere; equal neighbours merge, so V_k is the feasible set as a union of a few intervals.
+    // Its breakpoints are the finite region's ends of the full DP's (the same preimage arithmetic),
+    // so the feasibility verdict is the full DP's -- at a fraction of its cost (no cost steps).
     auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
     auto boxlo = [&](int k) { const double b = k == 0 ? lo0 : lo; return b - tw(b); };   // box of x_{k+1}
     auto boxhi = [&](int k) { const double b = k == 0 ? hi0 : hi; return b + tw(b); };
@@ -3125,7 +3138,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
 #define STP(i) do { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); spa[i] += n_ - spt; spt = n_; } while (0)
 #endif
     for (int k = H - 1; k >= 1; --k) {
-        const double A = cA[k], C = cC[k], q = cq[k];
+        const double A = cA[k], C = cC[k], q = feas_only ? 0.0 : cq[k];
         const double iA = 1.0 / A;
         const double* B = VB + (size_t)(k + 1) * STEP_CAP;
         const double* V = VV + (size_t)(k + 1) * STEP_CAP;
@@ -3281,10 +3294,10 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
                     if (xn >= B[0] && xn <= B[m]) {
                         int a = 0, b = m + 1;
                         while (a < b) { const int c = (a + b) >> 1; if (B[c] <= xn) a = c + 1; else b = c; }
-                        val = fma(cq[k], (double)lane, V[min(a - 1, m - 1)]);
+                        val = fma(feas_only ? 0.0 : cq[k], (double)lane, V[min(a - 1, m - 1)]);
                     }
                 } else {
-                    val = cq[k] * (double)lane;
+                    val = feas_only ? 0.0 : cq[k] * (double)lane;
                 }
             }
             const double vm = dpp_reduce(val, [](double a, double b) { return fmin(a, b); });
@@ -3317,7 +3330,6 @@ enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1, DM_NARROW = 2, DM_MID = 3 };
 
 template <bool EXPLICIT, int MODE, int NW = 1>
 DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int first_chain) {
-    static_assert(NW == 1 || MODE == DM_FRONT || MODE == DM_NARROW, "one wave per home in the mid / big launches");
     constexpr bool SECOND = MODE == DM_BUCKET || MODE == DM_MID;   // the bucketed DP + an exact big-front pass
     constexpr int NT = NW * WAVE;
     const int lane = threadIdx.x;
@@ -3434,7 +3446,10 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                                   reinterpret_cast<double*>(sb + nl.rl), reinterpret_cast<double*>(sb + nl.rh),
                                   reinterpret_cast<int*>(sw2), reinterpret_cast<int*>(sw2) + (size_t)16 * (STEP_CAP + 1),
                                   reinterpret_cast<double*>(sb + nl.bs)};
-                r = dp_steps<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, D.x, sx, sv, lane);
+                // feasibility first (cheap: the feasible set as a few intervals); a chain with no
+                // integer schedule -- the usual reason a home reaches this launch -- is decided there
+                r = dp_steps<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, D.x, sx, sv, lane, true);
+                if (r == 1) r = dp_steps<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, D.x, sx, sv, lane);
                 if (r >= 0) {
                     ok = r == 1;
                 } else {
@@ -3447,20 +3462,25 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
             }
             if (h.S == 6 && !(SECOND && rl_prices)) {
                 double* const wl = D.wl;
+                // (a multi-wave second launch: the exchange area of its mid / big layout, past the
+                // direct layout's arrays)
+                char* const xch = MODE == DM_FRONT ? D.xch
+                                : reinterpret_cast<char*>(smem) + (MODE == DM_MID ? mid_layout(H, a.d.sub_steps).xch
+                                                                                  : big_layout(H, a.d.sub_steps).xch);
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
-                                   wg, wl, wl + WAVE, wl + 2 * WAVE, MODE == DM_FRONT ? D.xch : nullptr};
+                                   wg, wl, wl + WAVE, wl + 2 * WAVE, xch};
                 if constexpr (MODE == DM_FRONT)
                     r = dp_front<6, NF_HOT, NF_HOT, NB_CAP, NTB_HOT, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
                 else
-                    r = dp_front<6, NF, NF_BOUND>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
+                    r = dp_front<6, NF, NF_BOUND, NB_CAP, NTB, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
 #ifdef DRAGG_FRONT_STATS2
                 // diagnostic: the T chain's fronts when the bound is the optimum itself
                 if (c0 && r == 1 && use_bound) {
                     double best = INFINITY;
-                    dp_front<6, NF, NF_BOUND>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound, INFINITY, &best);
+                    dp_front<6, NF, NF_BOUND, NB_CAP, NTB, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound, INFINITY, &best);
                     for (int k = lane; k < H; k += NT) D.x[k * 8 + S_PAD] = 0.0;
                     __syncthreads();
-                    r = dp_front<6, NF, NF_BOUND>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound, best);
+                    r = dp_front<6, NF, NF_BOUND, NB_CAP, NTB, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound, best);
                 }
 #endif
             }
@@ -3484,9 +3504,9 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 if (h.S == 6 && r != -2) {
                     // the exact pass with big fronts, bounded by the bucketed schedule's cost
                     double ub = INFINITY;
-                    if (ok) {
+                    if (ok) {                              // (every wave sums all stages)
                         double c = 0.0;
-                        for (int k = lane; k < H; k += NT) c += D.cq[k] * D.x[k * 8 + sv];
+                        for (int k = lane & (WAVE - 1); k < H; k += WAVE) c += D.cq[k] * D.x[k * 8 + sv];
                         ub = dpp_sum(c);
                     }
                     const BigLayout bl = MODE == DM_MID ? mid_layout(H, a.d.sub_steps) : big_layout(H, a.d.sub_steps);
@@ -3500,13 +3520,14 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                                        reinterpret_cast<unsigned long long*>(sb + bl.cb),
                                        reinterpret_cast<unsigned*>(sb + bl.mh), reinterpret_cast<unsigned*>(sb + bl.kl),
                                        reinterpret_cast<unsigned*>(sb + bl.flo), reinterpret_cast<unsigned*>(sb + bl.fhi),
-                                       D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE};
+                                       D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE,
+                                       sb + bl.xch};
                     __syncthreads();
                     // keeps the bucketed schedule in D.x unless it finds (and writes) the optimum
                     if constexpr (MODE == DM_MID)
-                        r2 = dp_front<6, NF_MID, NF_MID, NF_MID, NTB_MID>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
+                        r2 = dp_front<6, NF_MID, NF_MID, NF_MID, NTB_MID, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
                     else
-                        r2 = dp_front<6, NF_BIG, NF_BIG, NF_BIG, NTB_BIG>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
+                        r2 = dp_front<6, NF_BIG, NF_BIG, NF_BIG, NTB_BIG, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
                     if (MODE == DM_MID && r2 == -3) {         // past NF_MID: the big launch's 2,048-label fronts
                         if (lane == 0) blist[atomicAdd(blist + N, 1)] = home | (chain << 30);
                         return;
@@ -3700,10 +3721,10 @@ int mid_slots(int dev, int H, int S) {
     if (!slots_dev[dev]) {
         hipDeviceProp_t prop{};
         int per_cu = 0;
-        const void* k = (const void*)mpc_direct_kernel<EXPLICIT, DM_MID>;
+        const void* k = (const void*)mpc_direct_kernel<EXPLICIT, DM_MID, NW_MID>;
         if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
             hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, WAVE, (size_t)mid_layout(H, S).bytes) != hipSuccess)
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, NW_MID * WAVE, (size_t)mid_layout(H, S).bytes) != hipSuccess)
             return SECOND_SLOTS;
         slots_dev[dev] = max(1, min(MID_SLOTS_MAX, per_cu * prop.multiProcessorCount));
     }
@@ -3739,12 +3760,12 @@ int launch(const KArgs& a, hipStream_t s) {
     if (rc) return rc;
     // the deferred homes: the mid launch (fronts of 384 labels, many blocks), its overflows to the
     // big launch (2,048 labels, 2 blocks per CU), what no front DP can take to the step-function DP
-    const int rcm = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_MID>, attr[6], b,
-                                  min(N, mid_slots<EXPLICIT>(dev, a.d.horizon, a.d.sub_steps)), WAVE,
+    const int rcm = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_MID, NW_MID>, attr[6], b,
+                                  min(N, mid_slots<EXPLICIT>(dev, a.d.horizon, a.d.sub_steps)), NW_MID * WAVE,
                                   (size_t)mid_layout(a.d.horizon, a.d.sub_steps).bytes, s);
     if (rcm) return rcm;
-    const int rc2 = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_BUCKET>, attr[2], b, min(N, SECOND_SLOTS), WAVE,
-                                  (size_t)big_layout(a.d.horizon, a.d.sub_steps).bytes, s);
+    const int rc2 = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_BUCKET, NW_BIG>, attr[2], b, min(N, SECOND_SLOTS),
+                                  NW_BIG * WAVE, (size_t)big_layout(a.d.horizon, a.d.sub_steps).bytes, s);
     if (rc2) return rc2;
     return launch_kernel(mpc_direct_kernel<EXPLICIT, DM_NARROW, NT_STEPS / WAVE>, attr[5], b, min(N, NARROW_SLOTS),
                          NT_STEPS, (size_t)narrow_layout(a.d.horizon, a.d.sub_steps).bytes, s);
@@ -3820,25 +3841,26 @@ int dragg_mpc_kernel_info_get(const dragg_mpc_dims* dims, dragg_mpc_kernel_info*
     if (rc) return rc;
     if (!info) return DRAGG_E_ARG;
     *info = dragg_mpc_kernel_info{};
-    auto one = [&](const void* kern, int i, size_t lds) -> int {
+    auto one = [&](const void* kern, int i, size_t lds, int nt) -> int {
         hipFuncAttributes fa{};
         if (hipFuncGetAttributes(&fa, kern) != hipSuccess) return DRAGG_E_HIP;
         // the launches raise the dynamic LDS limit first (launch_kernel); so does the query
         if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return DRAGG_E_LDS;
         int blocks = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kern, WAVE, lds) != hipSuccess) return DRAGG_E_HIP;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kern, nt, lds) != hipSuccess) return DRAGG_E_HIP;
         info->vgprs[i] = fa.numRegs;
         info->scratch_bytes[i] = (int32_t)fa.localSizeBytes;
         info->lds_bytes[i] = (int32_t)lds;
-        info->threads[i] = WAVE;
+        info->threads[i] = nt;
         info->blocks_per_cu[i] = blocks;
         return DRAGG_OK;
     };
-    if (!direct_mode(dims)) return one((const void*)mpc_home_kernel<false>, 0, kernel_lds_bytes(dims));
-    int r = one((const void*)mpc_direct_kernel<false, DM_FRONT>, 0, kernel_lds_bytes(dims));
+    if (!direct_mode(dims)) return one((const void*)mpc_home_kernel<false>, 0, kernel_lds_bytes(dims), WAVE);
+    int r = one((const void*)mpc_direct_kernel<false, DM_FRONT>, 0, kernel_lds_bytes(dims), WAVE);
     if (r) return r;
-    return one((const void*)mpc_direct_kernel<false, DM_BUCKET>, 1, (size_t)big_layout(dims->horizon, dims->sub_steps).bytes);
+    return one((const void*)mpc_direct_kernel<false, DM_BUCKET, NW_BIG>, 1,
+               (size_t)big_layout(dims->horizon, dims->sub_steps).bytes, NW_BIG * WAVE);
 }
 
 int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, double* out3, void* stream) {

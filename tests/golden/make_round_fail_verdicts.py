@@ -18,7 +18,9 @@ rows, `mpc_calc.py:291-446`, T and Tw coupled through e T_{k+1}) is given to HiG
 Verdicts whose HiGHS run hit the time limit are recorded as undecided (None).
 Output: tests/golden/proven/round_fail_joint.json.gz (inputs + verdicts).
 
-Usage: python tests/golden/make_round_fail_verdicts.py CASES.json [workers] [rf_time_limit] [narrow_time_limit]"""
+Usage: python tests/golden/make_round_fail_verdicts.py CASES.json [workers] [rf_time_limit] [narrow_time_limit]
+       python tests/golden/make_round_fail_verdicts.py --from-journal [rf_time_limit] [narrow_time_limit]
+         (writes the fixture from the verdicts journalled so far, e.g. after a run was cut short)"""
 import gzip
 import json
 import multiprocessing as mp
@@ -76,7 +78,26 @@ def decide(args):
     return out
 
 
+def write_fixture(res, limit, nlimit):
+    res.sort(key=lambda r: (r["source"], r["t"], r["i"]))
+    path = os.path.join(HERE, "proven", "round_fail_joint.json.gz")
+    with gzip.open(path, "wt") as f:
+        json.dump({"cases": res, "time_limit": limit, "narrow_time_limit": nlimit,
+                   "note": "HiGHS on the reference's full model: round_fail = feasibility (zero objective), "
+                           "narrow = proven optimum; joint_feasible None = undecided within the limit"}, f)
+    n_rf = [r for r in res if r["status"] == "round_fail"]
+    print(f"{len(res)} cases; round_fail: {sum(r['joint_feasible'] is False for r in n_rf)} jointly infeasible, "
+          f"{sum(r['joint_feasible'] is True for r in n_rf)} jointly FEASIBLE, "
+          f"{sum(r['joint_feasible'] is None for r in n_rf)} undecided -> {path}")
+
+
 def main():
+    if sys.argv[1] == "--from-journal":
+        with open(os.path.join(HERE, "proven", "round_fail_joint.partial.jsonl")) as f:
+            res = list({(r["source"], r["t"], r["i"]): r for r in map(json.loads, f)}.values())
+        write_fixture(res, float(sys.argv[2]) if len(sys.argv) > 2 else 900.0,
+                      float(sys.argv[3]) if len(sys.argv) > 3 else 120.0)
+        return
     cases = json.load(open(sys.argv[1]))
     workers = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     limit = float(sys.argv[3]) if len(sys.argv) > 3 else 1800.0
@@ -92,16 +113,7 @@ def main():
             print(f"{r['source']} t={r['t']} i={r['i']} {r['status']}: joint feasible {r['joint_feasible']} "
                   f"(HiGHS {r['highs_status']}, {r['highs_seconds']:.1f}s), sequential {r['sequential_feasible']}",
                   flush=True)
-    res.sort(key=lambda r: (r["source"], r["t"], r["i"]))
-    path = os.path.join(HERE, "proven", "round_fail_joint.json.gz")
-    with gzip.open(path, "wt") as f:
-        json.dump({"cases": res, "time_limit": limit, "narrow_time_limit": nlimit,
-                   "note": "HiGHS on the reference's full model: round_fail = feasibility (zero objective), "
-                           "narrow = proven optimum; joint_feasible None = undecided within the limit"}, f)
-    n_rf = [r for r in res if r["status"] == "round_fail"]
-    print(f"{len(res)} cases; round_fail: {sum(r['joint_feasible'] is False for r in n_rf)} jointly infeasible, "
-          f"{sum(r['joint_feasible'] is True for r in n_rf)} jointly FEASIBLE, "
-          f"{sum(r['joint_feasible'] is None for r in n_rf)} undecided -> {path}")
+    write_fixture(res, limit, nlimit)
 
 
 if __name__ == "__main__":

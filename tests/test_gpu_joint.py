@@ -75,29 +75,49 @@ def test_round_fail_status_matches_the_joint_model(gpu):
             assert st == L.ST_OPTIMAL, (c["source"], c["t"], c["i"], L.STATUS_NAMES[st])
         else:
             n_inf += 1
-            assert st == L.ST_ROUND_FAIL, (c["source"], c["t"], c["i"], L.STATUS_NAMES[st])
+            # the failed solve's fallback may end in the reference's float(str[0]) ValueError
+            # (ERR_PARSE): the status the fallback leaves, the solve itself failed either way
+            assert st in (L.ST_ROUND_FAIL, L.ST_ERR_PARSE), (c["source"], c["t"], c["i"], L.STATUS_NAMES[st])
+            assert path & (3 << 13), (c["source"], c["t"], c["i"], hex(path))   # a chain decided it
     print(f"ROUND_FAIL cases: {n_inf} proven jointly infeasible (kernel: ROUND_FAIL), {n_feas} jointly feasible "
           f"(kernel: optimal), {n_und} undecided by HiGHS within its limit")
     assert n_inf + n_feas > 0
 
 
 def test_narrow_set_solves_against_the_joint_optimum(gpu):
+    """Narrow-set cases: with DRAGG_FLAG_EXACT the kernel's objective equals the exact sequential
+    optimum (oracle/thermal.py's assumption-free step-function DP + the LP, 1e-9 rel), never lies
+    below HiGHS's dual bound on the joint model, and equals HiGHS's joint optimum where it proved one
+    (1e-6).  The default build (bucketed schedule on these chains) is reported and bounded: never
+    below the optimum, the same status."""
     from dragg_amd import _lib as L
     cases = [c for c in _cases() if c["status"] != "round_fail"]
     if not cases:
         pytest.skip("no narrow-set case")
     res = _solve(cases, exact=True)            # DRAGG_FLAG_EXACT: the step-function DP
-    gaps = []
+    dflt = _solve(cases, exact=False)
+    gaps, dgaps, n_proven = [], [], 0
     for j, c in enumerate(cases):
         st, obj, path = res[j]
-        if c["joint_feasible"] is None:
+        where = (c["source"], c["t"], c["i"])
+        assert (st == L.ST_OPTIMAL) == bool(c["sequential_feasible"]), where
+        assert dflt[j][0] == st, where
+        if st != L.ST_OPTIMAL:
             continue
-        assert (st == L.ST_OPTIMAL) == bool(c["joint_feasible"]), (c["source"], c["t"], c["i"])
-        if st == L.ST_OPTIMAL and c.get("joint_opt") is not None:
+        seq = c["sequential_opt"]
+        assert abs(obj - seq) <= 1e-9 * max(1.0, abs(seq)), (where, obj, seq)
+        jb = c.get("joint_bound")
+        if jb is not None and np.isfinite(jb):
+            assert obj >= jb - 1e-6 * max(1.0, abs(jb)), (where, obj, jb)
+        if c.get("joint_opt") is not None:
+            n_proven += 1
             g = (obj - c["joint_opt"]) / max(1.0, abs(c["joint_opt"]))
-            assert g >= -1e-6, (c["source"], c["t"], c["i"], obj, c["joint_opt"])   # never below the optimum
+            assert abs(g) <= 1e-6, (where, obj, c["joint_opt"])
             gaps.append(g)
-    g = np.array(gaps)
-    print(f"narrow-set cases: {len(cases)}; gap to HiGHS's proven joint optimum: max {g.max() if len(g) else 0:.2e}, "
-          f"{int((g > 1e-6).sum())} above 1e-6")
-    assert len(g) == 0 or g.max() <= 1e-6
+        dg = (dflt[j][1] - obj) / max(1.0, abs(obj))
+        assert dg >= -1e-9, (where, dflt[j][1], obj)          # the bucketed schedule is never below
+        dgaps.append(dg)
+    d = np.array(dgaps)
+    print(f"narrow-set cases: {len(cases)}; exact mode = the sequential optimum on all, = HiGHS's proven joint "
+          f"optimum on {n_proven}; default build's bucketed schedules: max gap {d.max() if len(d) else 0:.2e}, "
+          f"{int((d > 1e-9).sum())} above 1e-9")
