@@ -2321,11 +2321,13 @@ DEV void w_to_lds(const FrontBufs& B, int lane, double wx, double wv) {
     B.wls[lane] = s;
 }
 // W(x) at a per-lane point from the LDS table: binary search, then the segment's line (its linear
-// extension outside [x_0, x_{m-1}], where the integer programme has no schedule anyway)
-DEV double w_eval(const FrontBufs& B, double x) {
+// extension outside [x_0, x_{m-1}], where the integer programme has no schedule anyway).  st0 = the
+// largest power of two <= m - 1 for a row of m points (w_st0): log2(m) dependent LDS reads, not 6
+// (rows of a tariff day hold a handful of points; the table past m is +inf)
+DEV int w_st0(int m) { return m <= 1 ? 0 : 1 << (31 - __builtin_clz((unsigned)(m - 1))); }
+DEV double w_eval(const FrontBufs& B, double x, int st0) {
     int i = 0;
-#pragma unroll
-    for (int st = WAVE / 2; st > 0; st >>= 1)
+    for (int st = st0; st > 0; st >>= 1)
         if (B.wlx[i + st] <= x) i += st;
     return fma(x - B.wlx[i], B.wls[i], B.wlv[i]);
 }
@@ -2431,8 +2433,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     auto set_count = [&](int j, int m) {
         if ((j & (WAVE - 1)) == lane) { if (j < WAVE) wc0 = m; else wc1 = m; }
     };
+    auto row_m = [&](int j) -> int { return j < WAVE ? read_lane(wc0, j) : read_lane(wc1, j - WAVE); };
     auto load_row = [&](int j) -> double2 {
-        const int m = j < WAVE ? read_lane(wc0, j) : read_lane(wc1, j - WAVE);
+        const int m = row_m(j);
         return lane < m ? B.wg[j * WAVE + lane] : make_double2(INFINITY, INFINITY);
     };
     // kf: the stage the DP continues from (rows W_{kf+1} .. W_H are built); the greedy upper bound
@@ -2518,7 +2521,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                 }
                 const double xc = fma(A, gx, fma(g, (double)lane, C));
                 double val = INFINITY;
-                if (lane <= SS && xc >= bl && xc <= bh) val = (double)lane * q + w_eval(B, xc);
+                if (lane <= SS && xc >= bl && xc <= bh) val = (double)lane * q + w_eval(B, xc, w_st0(row_m(k + 1)));
                 const double vm = dpp_reduce(val, [](double a, double b) { return fmin(a, b); });
                 if (!(vm < INFINITY)) { gok = false; break; }
                 const int bu = __ffsll((long long)__ballot(val == vm)) - 1;
@@ -2614,6 +2617,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             bl = fmax(bl, fma((double)B.flo[k + 1], hs, hb));
             bh = fmin(bh, fma((double)B.fhi[k + 1], hs, hb));
         }
+        const int wst = prune ? w_st0(row_m(k + 1)) : 0;   // W_{k+1}'s search depth
         // the children's state and cost ranges (widened past rounding) define the two bucket
         // grids of this stage.  A child's position in a range as a 32-bit fixed-point number
         // v = (key - lo) * NBK * 2^23 / (hi - lo) (one fma from the state) gives its bucket
@@ -2649,7 +2653,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             const double2 Li = fa[i];
             const double xc = fma(A, Li.x, fma(g, (double)u, C));
             const double cc = fma(q, (double)u, Li.y);
-            if (xc >= bl && xc <= bh && (!prune || cc + w_eval(B, xc) <= UBT)) {
+            if (xc >= bl && xc <= bh && (!prune || cc + w_eval(B, xc, wst) <= UBT)) {
                 const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
                 const unsigned cu = vc + 2u, kd = dn(vk);
                 atomicMin(&B.kb[min(NBK - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
@@ -2714,7 +2718,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             vk = fixp(fma(xc, kmul, kadd));
             vc = fixp(fma(cc, csc, cadd));
             bool keep = have && xc >= bl && xc <= bh;
-            if (keep && prune) keep = cc + w_eval(B, xc) <= UBT;
+            if (keep && prune) keep = cc + w_eval(B, xc, wst) <= UBT;
             if (keep && !nodom) {
                 const int kbk = min(NBK - 1, (int)(vk >> 23)), cbk = min(NBK - 1, (int)(vc >> 23));
                 const unsigned ku = vk + 2u, cd = dn(vc);
@@ -3328,8 +3332,13 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
 // bucketed DP and the big pass out of DM_FRONT keeps their registers and LDS out of the hot kernel.
 enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1, DM_NARROW = 2, DM_MID = 3 };
 
+// list entries: home | BK_DONE / BK_OK | deferred chain << 30 (homes < 2^28)
+constexpr int HOME_MASK = 0x0FFFFFFF;
+constexpr int BK_OK = 1 << 28;           // the bucketed DP found a schedule (in the solution rows)
+constexpr int BK_DONE = 1 << 29;         // the bucketed DP already ran for the deferred chain (mid -> big)
+
 template <bool EXPLICIT, int MODE, int NW = 1>
-DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int first_chain) {
+DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int first_chain, int eflags = 0) {
     constexpr bool SECOND = MODE == DM_BUCKET || MODE == DM_MID;   // the bucketed DP + an exact big-front pass
     constexpr int NT = NW * WAVE;
     const int lane = threadIdx.x;
@@ -3496,8 +3505,15 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30);
                 return;
             } else {
-                ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
-                              : dp_thermal<0>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
+                pf.mark(DRAGG_PH_INTEGER);
+                // a chain the mid launch handed over: its bucketed schedule is in the solution rows
+                // already (the mid pass overflowed without writing them), only the big pass is left
+                if (SECOND && chain == first_chain && (eflags & BK_DONE))
+                    ok = (eflags & BK_OK) != 0;
+                else
+                    ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
+                                  : dp_thermal<0>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
+                pf.mark(DRAGG_PH_ITER);                   // (round: the bucketed DP)
                 int r2 = r;
                 // the big pass, except for a feasible set narrower than one duty step (no
                 // dominance there: its fronts outgrow any capacity, measured)
@@ -3528,8 +3544,13 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                         r2 = dp_front<6, NF_MID, NF_MID, NF_MID, NTB_MID, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
                     else
                         r2 = dp_front<6, NF_BIG, NF_BIG, NF_BIG, NTB_BIG, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
+                    pf.mark(DRAGG_PH_POLISH);             // (round: the mid / big exact pass)
                     if (MODE == DM_MID && r2 == -3) {         // past NF_MID: the big launch's 2,048-label fronts
-                        if (lane == 0) blist[atomicAdd(blist + N, 1)] = home | (chain << 30);
+                        // (an RL-priced chain went straight to the bucketed DP: the big launch reuses
+                        // its schedule; other chains ran the regular front DP first and start over)
+                        if (lane == 0)
+                            blist[atomicAdd(blist + N, 1)] = home | (chain << 30) |
+                                                             (rl_prices ? BK_DONE | (ok ? BK_OK : 0) : 0);
                         return;
                     }
                     if (r2 == 1) ok = true;
@@ -3598,10 +3619,10 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
     const int* const list = reinterpret_cast<const int*>(reinterpret_cast<const char*>(a.p.workspace) + lo);
     const int cnt = min(list[a.d.n_homes], a.d.n_homes);
     for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
-        const int e = list[j];                      // home | deferred chain << 30
-        const int home = e & 0x3FFFFFFF, chain = (e >> 30) & 1;
+        const int e = list[j];                      // home | flags | deferred chain << 30
+        const int home = e & HOME_MASK, chain = (e >> 30) & 1;
         if (home >= a.d.n_homes) continue;
-        solve_direct<EXPLICIT, MODE, NW>(a, home, smem, blockIdx.x, chain);
+        solve_direct<EXPLICIT, MODE, NW>(a, home, smem, blockIdx.x, chain, e & (BK_DONE | BK_OK));
         __syncthreads();
     }
 }
@@ -3660,6 +3681,7 @@ size_t kernel_lds_bytes(const dragg_mpc_dims* d) {
 
 int check_dims(const dragg_mpc_dims* d) {
     if (!d || d->n_homes < 0 || d->horizon < 1 || d->sub_steps < 1 || d->dt < 1) return DRAGG_E_ARG;
+    if (d->n_homes > HOME_MASK) return DRAGG_E_ARG;                   // the deferred lists' home field
     if (d->int_mode < DRAGG_INT_ROUND || d->int_mode > DRAGG_INT_FAIL) return DRAGG_E_ARG;
     if (d->flags & ~DRAGG_FLAG_EXACT) return DRAGG_E_ARG;
     if (direct_mode(d) && d->sub_steps > 15) return DRAGG_E_ARG;     // 4-bit duty in the DP record
@@ -3696,6 +3718,10 @@ template <bool EXPLICIT>
 int hot_waves(int N, int dev, size_t lds) {
     const char* env = getenv("DRAGG_WAVES_PER_HOME");
     if (env && (env[0] == '1' || env[0] == '2' || env[0] == '4') && env[1] == 0) return env[0] - '0';
+    // measured (1,250 homes, the 8-GPU shard of the bench: 0.495 / 0.53 / 0.80 ms per step at 1 / 2 /
+    // 4 waves per home): a stage's fixed latency (ranges, scans, barriers) dominates its passes at
+    // these front sizes, so extra waves only add barriers -- one wave per home unless forced
+    if (!env) return 1;
     static int cap_dev[MAX_DEV][3] = {};                 // resident homes at 1, 2, 4 waves per home
     if (!cap_dev[dev][0]) {
         hipDeviceProp_t prop{};

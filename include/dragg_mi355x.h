@@ -194,9 +194,11 @@ typedef struct dragg_mpc_out {
 /* solver phases timed into dragg_mpc_out.cycles (diagnostic; NULL = not stamped) */
 enum dragg_phase {
     DRAGG_PH_SETUP = 0,   /* inputs, problem build, presolve              */
-    DRAGG_PH_ITER,        /* ADMM iterations (rhs, KKT solve, updates)    */
+    DRAGG_PH_ITER,        /* ADMM iterations (rhs, KKT solve, updates);   */
+                          /* int_mode round: the bucketed DP              */
     DRAGG_PH_FACTOR,      /* block-LDL' factorisations                    */
-    DRAGG_PH_POLISH,      /* exact basis polish                           */
+    DRAGG_PH_POLISH,      /* exact basis polish; int_mode round: the mid  */
+                          /* / big launch's exact front pass              */
     DRAGG_PH_CHECK,       /* residuals, certificate, rho adaptation       */
     DRAGG_PH_INTEGER,     /* integer duty-cycle DP                        */
     DRAGG_PH_WRITE,       /* objective, cleanup_and_finish, hash writes   */

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--month", type=int, default=1)
     ap.add_argument("--out", default=None)
     ap.add_argument("--world", type=int, default=1, help="rank 0's strided shard of a community sharded this wide")
+    ap.add_argument("--rl", action="store_true", help="bench.py's smooth RL reward price, a new one every step")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -38,7 +39,11 @@ def main():
                            seed=12, keep_history=False, rank=0, world=a.world)
     agg.batch.enable_phase_timing(True)
     cyc, st, it, kms = [], [], [], []
+    H = agg.batch.H
+    rng = np.random.default_rng(5)
     for _ in range(a.steps):
+        if a.rl:
+            agg.set_reward_price(rng.uniform(-0.02, 0.02) - 0.03 * np.cos(np.arange(H) / 3.0))
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         agg.run_iteration()
