@@ -1443,7 +1443,7 @@ __host__ __device__ inline size_t par_region_bytes(int N, int H) {
 // block of that persistent launch per slot
 __host__ __device__ inline size_t defer_offset(int N, int H) { return par_region_bytes(N, H) + (size_t)N * 8 * H * 8; }
 __host__ __device__ inline size_t w_region_offset(int N, int H) {
-    return (defer_offset(N, H) + (size_t)(N + 1) * sizeof(int) + 255) / 256 * 256;
+    return (defer_offset(N, H) + (size_t)(N + 2) * sizeof(int) + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t w_region_bytes(int N, int H) { return (size_t)N * (H + 1) * 64 * 16; }
 __host__ __device__ inline size_t big_region_offset(int N, int H) {
@@ -1463,7 +1463,7 @@ __host__ __device__ inline size_t narrow_list_offset(int N, int H) {
     return (big_region_offset(N, H) + big_region_bytes(H) + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t narrow_region_offset(int N, int H) {
-    return (narrow_list_offset(N, H) + (size_t)(N + 1) * sizeof(int) + 255) / 256 * 256;
+    return (narrow_list_offset(N, H) + (size_t)(N + 2) * sizeof(int) + 255) / 256 * 256;
 }
 // then the list of homes the mid launch hands to the big one ([N] i32 + length) and (256-aligned)
 // the mid launch's back-pointer rows [MID_SLOTS_MAX][H][NF_MID] u16
@@ -1471,7 +1471,7 @@ __host__ __device__ inline size_t mid_list_offset(int N, int H) {
     return (narrow_region_offset(N, H) + (size_t)NARROW_SLOTS * step_slot_bytes(H) + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t mid_region_offset(int N, int H) {
-    return (mid_list_offset(N, H) + (size_t)(N + 1) * sizeof(int) + 255) / 256 * 256;
+    return (mid_list_offset(N, H) + (size_t)(N + 2) * sizeof(int) + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t direct_workspace_bytes(int N, int H) {
     return mid_region_offset(N, H) + (size_t)MID_SLOTS_MAX * H * NF_MID * sizeof(uint16_t);
@@ -2442,6 +2442,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     // starts there from a label (gx0, c0) of the front (a feasible completion of it bounds the optimum)
     auto make_bound = [&](int kf, double gx0, double c0) -> bool {
         if (H >= 2 * WAVE) return false;                 // row counts held for 128 rows (a 32 h horizon)
+#ifdef DRAGG_STAGE_PROF
+        const unsigned long long mb_t0 = __builtin_amdgcn_s_memtime();
+#endif
         bool prune = true;
         {
             double bl = H == 1 ? lo0 : lo, bh = H == 1 ? hi0 : hi;
@@ -2477,25 +2480,22 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                 const unsigned long long bal = __ballot(in);
                 const int m2 = __popcll(bal) + 2;
                 if (m2 > WAVE) { prune = false; break; }
-                // compact through the LDS table (free here)
-                if (wid == 0 && in) {
-                    const int pos_ = 1 + __popcll(bal & ((1ull << lane) - 1ull));
-                    B.wlx[pos_] = nx;
-                    B.wlv[pos_] = nv;
-                }
-                if (tid == 0) {
-                    B.wlx[0] = dl; B.wlv[0] = vdl;
-                    B.wlx[m2 - 1] = dh; B.wlv[m2 - 1] = vdh;
-                }
-                __syncthreads();
-                wx = lane < m2 ? B.wlx[lane] : INFINITY;
-                wv = lane < m2 ? B.wlv[lane] : INFINITY;
+                // compact: the points inside (dl, dh) are a contiguous run of lanes (nx ascending),
+                // so the new row is that run shifted to lanes 1 .. m2 - 2 (one lane shuffle, no barrier)
+                const int first = bal ? __ffsll((long long)bal) - 1 : 0;
+                const int src = min(max(lane - 1 + first, 0), WAVE - 1);
+                const double sx_ = __shfl(nx, src), sv_ = __shfl(nv, src);
+                wx = lane == 0 ? dl : lane == m2 - 1 ? dh : lane < m2 ? sx_ : INFINITY;
+                wv = lane == 0 ? vdl : lane == m2 - 1 ? vdh : lane < m2 ? sv_ : INFINITY;
                 m = m2;
-                __syncthreads();
                 if (wid == 0 && lane < m) B.wg[j * WAVE + lane] = make_double2(wx, wv);
                 set_count(j, m);
             }
         }
+#ifdef DRAGG_STAGE_PROF
+        const unsigned long long mb_t1 = __builtin_amdgcn_s_memtime();
+        if (tid == 0) B.x[7 * 8 + S_PAD] += (double)(mb_t1 - mb_t0);
+#endif
         // (d) an upper bound: the cost of one feasible schedule, greedy in q u + W_{k+1}(x') (the
         //     labels' own arithmetic).  Children with cost + W > bound (+ a margin past rounding)
         //     cannot lead to the optimum and are dropped.
@@ -2505,10 +2505,14 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             qabs = dpp_sum(qabs);
             double gx = gx0, ub = c0;
             bool gok = true;
-            // (the W table is wave 0's to load and write; every wave reads it)
-            double2 cur = wid == 0 ? load_row(kf + 1) : make_double2(INFINITY, INFINITY);
+            // (the W table is wave 0's to load and write; every wave reads it.)  Rows in flight three
+            // stages ahead: a stage of this pass is far shorter than a global load's latency
+            const double2 NONE = make_double2(INFINITY, INFINITY);
+            double2 cur = wid == 0 ? load_row(kf + 1) : NONE;
+            double2 n1 = (wid == 0 && kf + 2 <= H) ? load_row(kf + 2) : NONE;
+            double2 n2 = (wid == 0 && kf + 3 <= H) ? load_row(kf + 3) : NONE;
             for (int k = kf; k < H && gok; ++k) {
-                double2 nxt = (wid == 0 && k + 2 <= H) ? load_row(k + 2) : make_double2(INFINITY, INFINITY);
+                const double2 n3 = (wid == 0 && k + 4 <= H) ? load_row(k + 4) : NONE;
                 if (wid == 0) w_to_lds(B, lane, cur.x, cur.y);
                 __syncthreads();
                 const double A = B.cA[k], C = B.cC[k], q = B.cq[k];
@@ -2527,7 +2531,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                 const int bu = __ffsll((long long)__ballot(val == vm)) - 1;
                 gx = read_lane(xc, bu);
                 ub = fma(q, (double)bu, ub);
-                cur = nxt;
+                cur = n1; n1 = n2; n2 = n3;
                 __syncthreads();
             }
             if (gok) UBT = ub + TOL_P * (1.0 + fabs(ub) + qabs);
@@ -2535,6 +2539,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             if (ub_ext < INFINITY) { UBT = fmin(UBT, ub_ext + TOL_P * (1.0 + fabs(ub_ext) + qabs)); gok = true; }
             if (!gok) prune = false;
         }
+#ifdef DRAGG_STAGE_PROF
+        if (tid == 0) B.x[8 * 8 + S_PAD] += (double)(__builtin_amdgcn_s_memtime() - mb_t1);
+#endif
         return prune;
     };
     bool prune = B.wg != nullptr && (use_bound || nodom) && make_bound(0, x0, 0.0);
@@ -2560,7 +2567,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
 #ifdef DRAGG_STAGE_PROF
     // diagnostic: shader-clock cycles per stage section (0 ranges, 1 pass 1, 2 scans, 3 pass 3,
     // 4 reductions / clears / W table, 5 stages), added into the S_PAD slots of stages 0..5
-    unsigned long long sp_acc[6] = {0, 0, 0, 0, 0, 0}, sp_t = __builtin_amdgcn_s_memtime();
+    unsigned long long sp_acc[7] = {0, 0, 0, 0, 0, 0, 0}, sp_t = __builtin_amdgcn_s_memtime();
 #define SP_MARK(i) do { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); sp_acc[i] += n_ - sp_t; sp_t = n_; } while (0)
 #endif
     for (int k = 0; k < H; ++k) {
@@ -2571,6 +2578,10 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         // a front past PRUNE_AT labels (a tariff boundary inside the horizon): build the LP
         // bound now and prune the remaining stages by it.  Only while the front fits the bounded
         // capacity (the W table's LDS follows it) -- and, when fa is that buffer, stays clear of it.
+#ifdef DRAGG_STAGE_PROF
+        const bool sp_trig = !tried && n > PRUNE_AT && n <= CAPB;
+        if (sp_trig) SP_MARK(0);
+#endif
         if (!tried && n > PRUNE_AT && n <= CAPB) {
             tried = true;
             // the rows from this stage on, the greedy bound from the front's cheapest label
@@ -2609,6 +2620,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             }
             __syncthreads();
         }
+#ifdef DRAGG_STAGE_PROF
+        if (sp_trig) SP_MARK(6);
+#endif
         const double A = B.cA[k], C = B.cC[k], q = B.cq[k];
         double bl = k == 0 ? lo0 : lo, bh = k == 0 ? hi0 : hi;
         bl -= tw(bl);
@@ -2837,7 +2851,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         n = nn;
     }
 #ifdef DRAGG_STAGE_PROF
-    if (tid == 0) for (int i = 0; i < 6; ++i) B.x[i * 8 + S_PAD] += (double)sp_acc[i];
+    if (tid == 0) for (int i = 0; i < 7; ++i) B.x[i * 8 + S_PAD] += (double)sp_acc[i];
 #endif
     // the cheapest final label (lowest index on ties)
     double best = INFINITY;
@@ -3607,23 +3621,29 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
 template <bool EXPLICIT, int MODE, int NW = 1>
 __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW ? 1 : 2) void mpc_direct_kernel(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
+    char* const ws = reinterpret_cast<char*>(a.p.workspace);
+    const int N = a.d.n_homes, H = a.d.horizon;
     if (MODE == DM_FRONT) {
-        if ((int)blockIdx.x < a.d.n_homes) solve_direct<EXPLICIT, MODE, NW>(a, blockIdx.x, smem, 0, 0);
+        if ((int)blockIdx.x < N) solve_direct<EXPLICIT, MODE, NW>(a, blockIdx.x, smem, 0, 0);
         return;
     }
-    // persistent: block b solves the listed homes b, b + gridDim.x, ... (its own scratch rows in
-    // the workspace: slot b); every block reaches the end of the list and exits
-    const size_t lo = MODE == DM_MID ? defer_offset(a.d.n_homes, a.d.horizon)
-                    : MODE == DM_BUCKET ? mid_list_offset(a.d.n_homes, a.d.horizon)
-                                        : narrow_list_offset(a.d.n_homes, a.d.horizon);
-    const int* const list = reinterpret_cast<const int*>(reinterpret_cast<const char*>(a.p.workspace) + lo);
-    const int cnt = min(list[a.d.n_homes], a.d.n_homes);
-    for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
+    // persistent: block b solves listed home b first, then takes the next ones off a shared counter
+    // (dynamic: a block that drew short homes takes more; measured on the RL workload: 38.2 -> 34.0
+    // ms per action against a static stride), each with its own scratch rows in the workspace (slot
+    // b); blocks past the list's length leave at once, every block reaches its end and exits
+    const size_t lo = MODE == DM_MID ? defer_offset(N, H) : MODE == DM_BUCKET ? mid_list_offset(N, H)
+                                                                             : narrow_list_offset(N, H);
+    int* const list = reinterpret_cast<int*>(ws + lo);
+    const int cnt = min(list[N], N);
+    __shared__ int take;
+    for (int j = blockIdx.x; j < cnt;) {
         const int e = list[j];                      // home | flags | deferred chain << 30
         const int home = e & HOME_MASK, chain = (e >> 30) & 1;
-        if (home >= a.d.n_homes) continue;
-        solve_direct<EXPLICIT, MODE, NW>(a, home, smem, blockIdx.x, chain, e & (BK_DONE | BK_OK));
+        if (home < N) solve_direct<EXPLICIT, MODE, NW>(a, home, smem, blockIdx.x, chain, e & (BK_DONE | BK_OK));
         __syncthreads();
+        if (threadIdx.x == 0) take = (int)gridDim.x + atomicAdd(list + N + 1, 1);
+        __syncthreads();
+        j = take;
     }
 }
 
@@ -3686,16 +3706,20 @@ int check_dims(const dragg_mpc_dims* d) {
     if (d->flags & ~DRAGG_FLAG_EXACT) return DRAGG_E_ARG;
     if (direct_mode(d) && d->sub_steps > 15) return DRAGG_E_ARG;     // 4-bit duty in the DP record
     if (direct_mode(d) && !direct_fits(d->horizon)) return DRAGG_E_HORIZON;
-    if (kernel_lds_bytes(d) > 160 * 1024) return DRAGG_E_HORIZON;
-    if (direct_mode(d) && big_layout(d->horizon, d->sub_steps).bytes > 160 * 1024) return DRAGG_E_HORIZON;
-    if (direct_mode(d) && narrow_layout(d->horizon, d->sub_steps).bytes > 160 * 1024) return DRAGG_E_HORIZON;
+    if (kernel_lds_bytes(d) > 160 * 1024 - 256) return DRAGG_E_HORIZON;
+    if (direct_mode(d) && big_layout(d->horizon, d->sub_steps).bytes > 160 * 1024 - 256) return DRAGG_E_HORIZON;
+    if (direct_mode(d) && narrow_layout(d->horizon, d->sub_steps).bytes > 160 * 1024 - 256) return DRAGG_E_HORIZON;
     return DRAGG_OK;
 }
+
+// the dynamic LDS limit the launches raise: the 160 KB of a CU less room for the kernels' static
+// LDS (the persistent launches' take slot)
+constexpr int LDS_DYN_MAX = 160 * 1024 - 256;
 
 template <typename K>
 int launch_kernel(K kern, int& attr_state, const KArgs& a, int blocks, int nt, size_t lds, hipStream_t s) {
     if (!attr_state) {
-        if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+        if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DYN_MAX) !=
             hipSuccess)
             return DRAGG_E_LDS;
         attr_state = 1;
@@ -3731,7 +3755,7 @@ int hot_waves(int N, int dev, size_t lds) {
                             (const void*)mpc_direct_kernel<EXPLICIT, DM_FRONT, 4>};
         for (int i = 0; i < 3; ++i) {
             int per_cu = 0;
-            if (hipFuncSetAttribute(k[i], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+            if (hipFuncSetAttribute(k[i], hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DYN_MAX) != hipSuccess ||
                 hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k[i], WAVE << i, lds) != hipSuccess)
                 return 1;
             cap_dev[dev][i] = max(1, per_cu * prop.multiProcessorCount);
@@ -3749,7 +3773,7 @@ int mid_slots(int dev, int H, int S) {
         int per_cu = 0;
         const void* k = (const void*)mpc_direct_kernel<EXPLICIT, DM_MID, NW_MID>;
         if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
-            hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+            hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DYN_MAX) != hipSuccess ||
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, NW_MID * WAVE, (size_t)mid_layout(H, S).bytes) != hipSuccess)
             return SECOND_SLOTS;
         slots_dev[dev] = max(1, min(MID_SLOTS_MAX, per_cu * prop.multiProcessorCount));
@@ -3771,9 +3795,10 @@ int launch(const KArgs& a, hipStream_t s) {
     int* const len = reinterpret_cast<int*>(wsb + defer_offset(N, a.d.horizon)) + N;
     int* const nlen = reinterpret_cast<int*>(wsb + narrow_list_offset(N, a.d.horizon)) + N;
     int* const blen = reinterpret_cast<int*>(wsb + mid_list_offset(N, a.d.horizon)) + N;
-    if (hipMemsetAsync(len, 0, sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
-    if (hipMemsetAsync(nlen, 0, sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
-    if (hipMemsetAsync(blen, 0, sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
+    // (each list's length and the persistent launch's take counter after it)
+    if (hipMemsetAsync(len, 0, 2 * sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
+    if (hipMemsetAsync(nlen, 0, 2 * sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
+    if (hipMemsetAsync(blen, 0, 2 * sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
     const size_t lds = kernel_lds_bytes(&a.d);
     const int nw = hot_waves<EXPLICIT>(N, dev, lds);
     const char* fs = getenv("DRAGG_FORCE_STEP_DP");
@@ -3871,7 +3896,7 @@ int dragg_mpc_kernel_info_get(const dragg_mpc_dims* dims, dragg_mpc_kernel_info*
         hipFuncAttributes fa{};
         if (hipFuncGetAttributes(&fa, kern) != hipSuccess) return DRAGG_E_HIP;
         // the launches raise the dynamic LDS limit first (launch_kernel); so does the query
-        if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+        if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DYN_MAX) != hipSuccess)
             return DRAGG_E_LDS;
         int blocks = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kern, nt, lds) != hipSuccess) return DRAGG_E_HIP;

@@ -20,11 +20,11 @@ def offsets(N, H):
     r = lambda x: (x + 255) // 256 * 256  # noqa: E731
     par = r(N * H * 336 * 2)
     defer = par + N * 8 * H * 8
-    w_off = r(defer + (N + 1) * 4)
+    w_off = r(defer + (N + 2) * 4)
     big = r(w_off + N * (H + 1) * 64 * 16)
     nl = r(big + 512 * H * 2048 * 2)
     slot = (2 * (H + 1) * 16384 + 2 * 16 * 16385) * 8 + (16 + 16 * 15) * 16385 * 4
-    nr = r(nl + (N + 1) * 4)
+    nr = r(nl + (N + 2) * 4)
     ml = r(nr + 8 * slot)
     return defer, ml, nl
 

@@ -35,11 +35,12 @@ acc = []
 for t in range(a.steps):
     agg.run_iteration()
     torch.cuda.synchronize()
-    x = agg.batch.workspace.view(torch.uint8)[par:par + N * 8 * H * 8].view(torch.float64).view(N, H, 8)[:, :6, 7]
+    x = agg.batch.workspace.view(torch.uint8)[par:par + N * 8 * H * 8].view(torch.float64).view(N, H, 8)[:, :9, 7]
     st = agg.batch.status.cpu().numpy()
     v = x.cpu().numpy().copy()
     acc.append(v[st == L.ST_OPTIMAL])
-acc = np.concatenate(acc)                      # [solves][6]
+acc = np.concatenate(acc)                      # [solves][7]
+acc[:, 0] += acc[:, 6]                         # (section 0 = ranges + the bound trigger; 6 = the trigger)
 per_stage = acc[:, :5] / np.maximum(acc[:, 5:6], 1)
 tot = acc[:, :5].sum(1)
 slow = tot >= np.percentile(tot, 99)
@@ -48,6 +49,13 @@ res = {"homes": N, "world": a.world, "steps": a.steps,
        "cycles_per_stage_mean": dict(zip(names, per_stage.mean(0).round(1).tolist())),
        "cycles_per_stage_slowest1pct": dict(zip(names, per_stage[slow].mean(0).round(1).tolist())),
        "stages_per_solve_mean": float(acc[:, 5].mean()),
+       "trigger_cycles_per_solve_mean": float(acc[:, 6].mean()),
+       "trigger_cycles_per_solve_slowest1pct": float(acc[slow, 6].mean()),
+       "trigger_share_of_dp": float(acc[:, 6].sum() / max(1.0, tot.sum())),
+       "bound_backward_cycles_per_solve_mean": float(acc[:, 7].mean()),
+       "bound_greedy_cycles_per_solve_mean": float(acc[:, 8].mean()),
+       "bound_rows_per_solve_mean": None,
+       "trigger_share_of_dp_slowest1pct": float(acc[slow, 6].sum() / max(1.0, tot[slow].sum())),
        "dp_cycles_per_solve_pct": {str(q): float(np.percentile(tot, q)) for q in (50, 90, 99, 100)}}
 print(json.dumps(res, indent=1))
 if a.out:
