@@ -11,7 +11,7 @@ OUT=gpurun_out/cpu_$TAG
 mkdir -p $OUT
 ( while sleep 50; do echo "tick $(date +%T)"; done ) &
 HB=$!
-timeout -k 10 $((WALL + 120)) python3 -u bench.py --cpu-only --cpu-seconds $WALL --cpu-home-steps 1000 --cpu-milp-limit 300 "$@" > $OUT/cpu_baseline_full.json 2> $OUT/cpu.err
+timeout -k 10 $((WALL + 120)) python3 -u bench.py --cpu-only --cpu-seconds $WALL --cpu-home-steps ${HOME_STEPS:-1000} --cpu-milp-limit 300 "$@" > $OUT/cpu_baseline_full.json 2> $OUT/cpu.err
 rc=$?
 kill $HB
 cut -c1-400 $OUT/cpu_baseline_full.json
