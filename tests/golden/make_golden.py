@@ -77,10 +77,13 @@ class _NoiseRandom:
 
     def __init__(self, seed, index_of, log):
         self.seed, self.index_of, self.log = seed, index_of, log
+        self.cp = None
 
     def randn(self, *shape):
         me = inspect.currentframe().f_back.f_locals["self"]
         hidx = self.index_of[me.name]
+        if self.cp is not None:
+            self.cp.CURRENT_HOME[0] = hidx          # (GOLDEN_OWN runs: the shim's solve limits)
         draw = np.random.default_rng([self.seed, hidx, int(me.timestep)]).standard_normal(shape)
         self.log[(me.name, int(me.timestep))] = draw.copy()
         return draw
@@ -131,7 +134,9 @@ def run(name, sc, hook=None):
     import pathos.pools as pp  # refshim
     del pp.EXTRA[:]
     index_of, noise_log, records = {}, {}, pp.EXTRA
-    mc.np = _NumpyProxy(_NoiseRandom(sc["seed"], index_of, noise_log))
+    rnd = _NoiseRandom(sc["seed"], index_of, noise_log)
+    rnd.cp = cp
+    mc.np = _NumpyProxy(rnd)
     record_t = set(sc["record_t"])
 
     orig_cleanup = mc.MPCCalc.cleanup_and_finish
@@ -233,7 +238,10 @@ def run(name, sc, hook=None):
     shutil.rmtree(work, ignore_errors=True)
     sys.path.remove(os.path.join(HERE, "refshim"))
     sys.path.remove(REF)
-    path = os.path.join(os.environ.get("GOLDEN_OUT_DIR", HERE), f"{name}.json.gz")
+    if cp.OWN is not None:                  # a part of a run split by home: only its homes' records
+        records[:] = [r for r in records if r["home"] in cp.OWN]
+        out["params"]["own"] = sorted(cp.OWN)
+    path = os.path.join(os.environ.get("GOLDEN_OUT_DIR", HERE), f"{name}{os.environ.get('GOLDEN_PART', '')}.json.gz")
     with gzip.open(path, "wt") as f:
         json.dump(out, f, separators=(",", ":"))
     nst = {}

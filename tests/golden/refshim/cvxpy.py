@@ -16,6 +16,13 @@ in `Problem.last_record`, so the harness can emit golden vectors.
 import numpy as np
 from scipy.optimize import milp, LinearConstraint, Bounds
 
+# the home whose problem is being solved (set by the harness's noise hook, per worker process), and
+# GOLDEN_OWN: the home indices this run proves (a run split over processes by home: a home's closed
+# loop depends on its own solves only, so each process proves its homes and solves the others fast)
+CURRENT_HOME = [None]
+_OWN = __import__("os").environ.get("GOLDEN_OWN")
+OWN = None if not _OWN else {int(v) for v in _OWN.split(",")}
+
 GLPK_MI = "GLPK_MI"
 GLPK = "GLPK"
 ECOS = "ECOS"
@@ -270,6 +277,9 @@ class Problem:
 
     @staticmethod
     def _run(cobj, A_eq, b_eq, A_ub, b_ub, integ):
+        lim, gap = Problem.time_limit, Problem.mip_rel_gap
+        if OWN is not None and CURRENT_HOME[0] not in OWN:     # another process proves this home
+            lim, gap = float(__import__("os").environ.get("GOLDEN_OTHER_LIMIT", "2")), 1e-2
         cons = []
         if A_eq.shape[0]:
             cons.append(LinearConstraint(A_eq, b_eq, b_eq))
@@ -277,8 +287,7 @@ class Problem:
             cons.append(LinearConstraint(A_ub, -np.inf, b_ub))
         return milp(cobj, constraints=cons, integrality=integ,
                     bounds=Bounds(-np.inf, np.inf),
-                    options={"time_limit": Problem.time_limit, "mip_rel_gap": Problem.mip_rel_gap,
-                             "presolve": True})
+                    options={"time_limit": lim, "mip_rel_gap": gap, "presolve": True})
 
     def solve(self, solver=None, verbose=False, **kw):
         vars_, order, off, cobj, A_eq, b_eq, A_ub, b_ub, integ, c0 = self._assemble()
