@@ -2504,13 +2504,17 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             for (int k = lane; k < H; k += WAVE) qabs += fabs(B.cq[k]) * SS;
             qabs = dpp_sum(qabs);
             double gx = gx0, ub = c0;
-            bool gok = true;
+            // a caller's bound (the cost of a schedule it has: the bucketed DP's in the mid / big
+            // launches) makes the greedy pass unnecessary (RL action 33.7 -> 30.5 ms).  (Last step's
+            // plan shifted by a stage as the hot launch's bound, measured: looser than the greedy
+            // one, driver window 1.45 -> 1.55 ms)
+            bool gok = !(ub_ext < INFINITY);
             // (the W table is wave 0's to load and write; every wave reads it.)  Rows in flight three
             // stages ahead: a stage of this pass is far shorter than a global load's latency
             const double2 NONE = make_double2(INFINITY, INFINITY);
-            double2 cur = wid == 0 ? load_row(kf + 1) : NONE;
-            double2 n1 = (wid == 0 && kf + 2 <= H) ? load_row(kf + 2) : NONE;
-            double2 n2 = (wid == 0 && kf + 3 <= H) ? load_row(kf + 3) : NONE;
+            double2 cur = (wid == 0 && gok) ? load_row(kf + 1) : NONE;
+            double2 n1 = (wid == 0 && gok && kf + 2 <= H) ? load_row(kf + 2) : NONE;
+            double2 n2 = (wid == 0 && gok && kf + 3 <= H) ? load_row(kf + 3) : NONE;
             for (int k = kf; k < H && gok; ++k) {
                 const double2 n3 = (wid == 0 && k + 4 <= H) ? load_row(k + 4) : NONE;
                 if (wid == 0) w_to_lds(B, lane, cur.x, cur.y);
