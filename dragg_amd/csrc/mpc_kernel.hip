@@ -3651,6 +3651,14 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
     }
 }
 
+// the three device lists' (length, take counter) pairs to zero before a step's launches
+__global__ void reset_lists_kernel(int* a, int* b, int* c) {
+    const int i = threadIdx.x;
+    if (i < 2) a[i] = 0;
+    else if (i < 4) b[i - 2] = 0;
+    else if (i < 6) c[i - 4] = 0;
+}
+
 // collect_data's three sums (aggregator.py:728-755) in one 1024-thread block: 16 waves of
 // independent loads (a step's sums are a latency-bound 240 KB read at 10k homes), then a wave
 // reduction and a pass over the 16 wave partials
@@ -3799,10 +3807,10 @@ int launch(const KArgs& a, hipStream_t s) {
     int* const len = reinterpret_cast<int*>(wsb + defer_offset(N, a.d.horizon)) + N;
     int* const nlen = reinterpret_cast<int*>(wsb + narrow_list_offset(N, a.d.horizon)) + N;
     int* const blen = reinterpret_cast<int*>(wsb + mid_list_offset(N, a.d.horizon)) + N;
-    // (each list's length and the persistent launch's take counter after it)
-    if (hipMemsetAsync(len, 0, 2 * sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
-    if (hipMemsetAsync(nlen, 0, 2 * sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
-    if (hipMemsetAsync(blen, 0, 2 * sizeof(int), s) != hipSuccess) return DRAGG_E_HIP;
+    // each list's length and the persistent launch's take counter after it, in one tiny launch
+    // (three 8-byte memsets cost three fills: ~13 us of a 0.49 ms step at 1,250 homes)
+    hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, nlen, blen);
+    if (hipGetLastError() != hipSuccess) return DRAGG_E_HIP;
     const size_t lds = kernel_lds_bytes(&a.d);
     const int nw = hot_waves<EXPLICIT>(N, dev, lds);
     const char* fs = getenv("DRAGG_FORCE_STEP_DP");
