@@ -1,0 +1,53 @@
+"""The committed measurement is reproducible from the committed profiles:
+profiles/r03/traffic_*.json recompute from the raw rocprofv3 passes under profiles/r03/*_prof
+(tools/make_traffic.py), and the committed bench lines' kernel time and derived rooflines agree with
+the profile of the same command and window (within 5 %)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = os.path.join(ROOT, "profiles", "r03")
+
+CASES = [
+    ("driver", ["--steps", "20", "--warmup", "5"]),
+    ("rl", ["--steps", "6", "--warmup", "1", "--workload", "rl", "--rl-price", "smooth", "--forecast-horizon", "1"]),
+]
+
+
+@pytest.mark.parametrize("name,args", CASES)
+def test_traffic_recomputes_from_raw_passes(name, args, tmp_path):
+    prof = os.path.join(P, f"{name}_prof")
+    if not os.path.isdir(prof):
+        pytest.skip("no raw profile passes")
+    out = tmp_path / "t.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "make_traffic.py"), "--prof", prof, "--out", str(out)]
+                   + args, check=True, capture_output=True)
+    got = json.load(open(out))
+    ref = json.load(open(os.path.join(P, f"traffic_{name}.json")))
+    assert got["workload"] == ref["workload"]
+    assert got["kernel_ms_per_step"] == pytest.approx(ref["kernel_ms_per_step"], rel=1e-12)
+    assert got["bytes_per_step"] == pytest.approx(ref["bytes_per_step"], rel=1e-12)
+    for k, v in ref["sq_per_step"].items():
+        assert got["sq_per_step"][k] == pytest.approx(v, rel=1e-12), k
+
+
+@pytest.mark.parametrize("name", ["driver", "rl"])
+def test_bench_line_agrees_with_its_profile(name):
+    sys.path.insert(0, ROOT)
+    import bench
+    line = json.load(open(os.path.join(P, f"bench_{name}_line.json")))
+    tj = json.load(open(os.path.join(P, f"traffic_{name}.json")))
+    r = line["roofline"]
+    assert r["profile_key"] == tj["workload"]                     # the same command and window
+    assert r["kernel_ms"] == pytest.approx(tj["kernel_ms_per_step"], rel=0.05)
+    # the derived rooflines recompute from the profile's own counters and kernel time
+    ks = tj["kernel_ms_per_step"] * 1e-3
+    cyc = bench.valu_cycles(tj["sq_per_step"])
+    assert line["roofline_valu"]["frac"] == pytest.approx(cyc / ks / (bench.N_SIMD * bench.CLOCK), rel=1e-9)
+    assert r["traffic"] == pytest.approx(tj["bytes_per_step"] / (r["kernel_ms"] * 1e-3) / 1e9, rel=1e-9)
+    if "dp_work" in line:
+        assert line["dp_work"]["achieved"] == pytest.approx(tj["front_stats"]["children_per_step"] / ks / 1e9, rel=1e-9)
