@@ -128,7 +128,9 @@ def test_closed_loop_configs0_against_proven_optima(gpu):
     noise = {(r["t"], r["name"]): r["noise"] for r in d["records"]}
     dev = DeviceAggregator(homes, oat, ghi, tou, 0, T, reward_price=rp, seed=p["seed"])
     for t in range(T):
-        z = np.stack([noise[(t, h["name"])] for h in homes], axis=1)
+        # (a partial fixture holds no records of the homes its missing parts proved: any draw does
+        # for them, their series are not compared)
+        z = np.stack([np.asarray(noise.get((t, h["name"]), np.zeros(H))) for h in homes], axis=1)
         dev.run_iteration(torch.tensor(z))
         dev.collect_data()
     torch.cuda.synchronize()
