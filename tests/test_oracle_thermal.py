@@ -135,3 +135,38 @@ def test_exact_fixture_recomputes():
             assert (opt is None) == (e["opt_obj"] is None), (name, i)
             if opt is not None:
                 assert opt == pytest.approx(e["opt_obj"], rel=1e-12, abs=1e-12), (name, i)
+
+
+def test_exact_milp_on_the_proven_configs0_loop():
+    """The configs[0] reference loop re-run to proven optimality (tests/golden/proven/c1_h24_proven.json.gz,
+    HiGHS gap 0): on a sample of its solves the exact MILP optimum equals every proven optimum (2e-6),
+    is None on every proven-infeasible record and never above a time-limited incumbent -- the CPU
+    side of test_gpu_closed_loop.py's proven-loop test."""
+    import gzip
+    import json
+    import os
+    path = os.path.join(F.GOLDEN, "proven", "c1_h24_proven.json.gz")
+    if not os.path.exists(path):
+        pytest.skip("no proven configs[0] fixture")
+    with gzip.open(path, "rt") as f:
+        d = json.load(f)
+    homes = {h["name"]: h for h in d["homes"]}
+    n = dict(proven=0, infeasible=0, incumbent=0)
+    for r in d["records"][::16]:
+        hc = M.home_const(homes[r["name"]])
+        opt = TH.exact_milp(hc, _si(r))
+        ms, mo = r["milp_status"], r["milp_obj"]
+        if ms == 2:
+            n["infeasible"] += 1
+            assert opt is None, (r["name"], r["t"])
+        elif mo is not None:
+            assert opt is not None, (r["name"], r["t"])
+            rel = (opt - mo) / max(1.0, abs(mo))
+            if ms == 0:
+                n["proven"] += 1
+                assert abs(rel) <= 2e-6, (r["name"], r["t"], opt, mo)
+            else:
+                n["incumbent"] += 1
+                assert rel <= 2e-6, (r["name"], r["t"], opt, mo)
+    assert n["proven"] >= 50
+    print(n)
