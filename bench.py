@@ -16,10 +16,17 @@ A "step" is one closed-loop timestep of the whole community: one solver launch p
 24-byte RCCL all-reduce.  The community is sharded over the ranks (strong scaling: --homes
 is the community size).  `value` = homes x timed steps / max-over-ranks wall time.
 
+Ranks: under torch.distributed.run (WORLD_SIZE set) each process is one rank and --gpus must
+equal WORLD_SIZE; a plain `python bench.py --gpus N` starts the N rank processes itself (child
+processes, before any GPU use) and exits with their status.  DRAGG_BENCH_BACKEND=gloo rehearses
+N ranks on fewer GPUs (ranks share devices round-robin).
+
 Also reported (rank 0): `roofline` of the solver kernel (algorithmic HBM bytes per launch
 over the launch time measured with HIP events on the launch stream), `cpu_baseline` (N = 1
 only): the repo's CPU restatement of the reference solve (oracle/, HiGHS MILP in place of
-GLPK_MI) timed on this host's cores on a bounded sample of the same workload.
+GLPK_MI) on this host's cores -- the committed >= 1,000-home-step run of the same workload
+(`bench.py --cpu-only`, profiles/*/cpu_baseline_*.json, labelled as committed) with this run's
+own bounded sample beside it (`in_run_sample`).
 """
 import argparse
 import json
@@ -47,6 +54,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = the host cores this job may use")
     ap.add_argument("--cpu-home-steps", type=int, default=1000,
                     help="CPU baseline sample size (home-steps; stopped early at --cpu-seconds of wall time)")
+    ap.add_argument("--cpu-steps-per-home", type=int, default=4,
+                    help="CPU baseline: closed-loop steps per sampled home from t = 0 (configs[0] in full: 96 "
+                         "with --homes 20 --cpu-home-steps 1920)")
     ap.add_argument("--cpu-milp-limit", type=float, default=300.0,
                     help="HiGHS time limit per CPU solve; solves that reach it are counted separately")
     ap.add_argument("--cpu-only", action="store_true",
@@ -64,6 +74,8 @@ def parse(argv=None):
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic: time rank 0's strided shard of the community sharded this many ways, on "
                          "one GPU without the collectives (the per-GPU load of an N-GPU strong-scaling run)")
+    ap.add_argument("--exact", action="store_true",
+                    help="DRAGG_FLAG_EXACT (diagnostic): every chain the front DPs cannot take goes to the step-function DP")
     ap.add_argument("--no-history", action="store_true",
                     help="skip the per-step history write (collected_data); a configs[2] run keeps it")
     ap.add_argument("--keep-crashing-homes", action="store_true",
@@ -132,8 +144,10 @@ def _cpu_worker(args):
             if (deadline and time.time() >= deadline) or n >= quota:
                 return n, times, limited[0]
             t0 = time.time()
+            # (RL workload: the reward price of action t, redis_set_current_values aggregator.py:671-675)
+            env_t = dict(env, reward_price=env["rp_steps"][t]) if env.get("rp_steps") is not None else env
             try:
-                M.run_home_step(hc, t, hsh, env, rng.standard_normal(hc.H), solver=solver)
+                M.run_home_step(hc, t, hsh, env_t, rng.standard_normal(hc.H), solver=solver)
             except Exception:
                 break
             times.append(time.time() - t0)
@@ -156,7 +170,8 @@ def cpu_baseline(homes, env, seconds, workers, home_steps, milp_limit=300.0, ste
     n_homes = max(workers, -(-home_steps // steps_per_home))
     picks = [homes[(i * 7919) % len(homes)] for i in range(n_homes)]
     per = [picks[w::workers] for w in range(workers)]
-    quota = -(-home_steps // workers)
+    # a sample covering every step of every home (configs[0] in full) runs each home's whole loop
+    quota = -(-home_steps // workers) if n_homes * steps_per_home > home_steps else 1 << 40
     t0 = time.time()
     with mp.get_context("fork").Pool(workers) as pool:
         res = pool.map(_cpu_worker, [(p, env, deadline, milp_limit, steps_per_home, quota) for p in per])
@@ -184,19 +199,46 @@ def cpu_baseline(homes, env, seconds, workers, home_steps, milp_limit=300.0, ste
                       f"whole workload (home solves are independent)"}
 
 
-def committed_cpu_baseline():
-    """The committed full CPU-baseline run (bench.py --cpu-only on the GPU box, >= 1,000
-    home-steps): profiles/*/cpu_baseline_full.json, newest first."""
+def cpu_workload_key(n_total, Hh, dt, month, rl_price=None):
+    """The identity of a CPU-baseline workload (bench.py --cpu-only writes it into its JSON)."""
+    w = f"{n_total} homes, H={Hh * dt} ({Hh} h), {60 // dt}-min steps, month {month}, "
+    if rl_price:
+        return w + f"run_rl_agg reward price ({rl_price}), closed loop from t = 0"
+    return w + "run_rbo_mpc closed loop from t = 0"
+
+
+def committed_cpu_baseline(workload=None):
+    """The committed full CPU-baseline run of this workload (bench.py --cpu-only on the GPU box,
+    >= 1,000 home-steps): profiles/*/cpu_baseline_*.json whose `workload` is this one,
+    newest round first."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "cpu_baseline_full.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "cpu_baseline_*.json")), reverse=True):
         try:
             with open(f) as fh:
                 d = json.load(fh)
         except (OSError, ValueError):
             continue
-        return {k: d.get(k) for k in ("value", "unit", "cores", "home_steps", "time_limited_solves",
-                                     "median_solve_s", "wall_s", "workload")} | {"source": os.path.relpath(f, ROOT)}
+        if workload is not None and d.get("workload") != workload:
+            continue
+        if (d.get("home_steps") or 0) < 1000:
+            continue
+        return {k: d.get(k) for k in ("value", "unit", "cores", "kind", "home_steps", "time_limited_solves",
+                                     "median_solve_s", "wall_s", "workload", "sample")} | {"source": os.path.relpath(f, ROOT)}
     return None
+
+
+def headline_cpu_baseline(full, sample):
+    """`cpu_baseline` of the line: the committed >= 1,000-home-step run of this workload (BASELINE.md:
+    35-37; a bounded in-run sample over-represents short solves), labelled as committed, with this run's
+    own bounded sample beside it; without a committed run, the in-run sample."""
+    if full is None:
+        return sample
+    out = dict(full)
+    out["measured_in_this_run"] = False
+    out["sample"] = (f"COMMITTED run ({full['source']}, bench.py --cpu-only on a GPU box of this pool): "
+                     + (full.get("sample") or ""))
+    out["in_run_sample"] = sample
+    return out
 
 
 # ----------------------------------------------------------------------------- roofline
@@ -301,10 +343,9 @@ def occupancy(batch):
     """Registers, spills, LDS and resident homes per CU of the step's launches, as the code object
     and the runtime report them on this device (dragg_mpc_kernel_info_get)."""
     from dragg_amd import _lib as L
-    hot, second = L.kernel_info(batch.dims)
-    return {"hot": hot | {"waves_per_simd": hot["blocks_per_cu"] / 4.0},
-            "second": second,
-            "source": "hipFuncGetAttributes + hipOccupancyMaxActiveBlocksPerMultiprocessor (live, this device)"}
+    info = L.kernel_info(batch.dims)
+    info["hot"]["waves_per_simd"] = info["hot"]["blocks_per_cu"] * info["hot"]["threads"] / 64 / 4.0
+    return info | {"source": "hipFuncGetAttributes + hipOccupancyMaxActiveBlocksPerMultiprocessor (live, this device)"}
 
 
 def traffic_key(n_total, H, dt, month, int_mode, world, workload="rbo", steps=None, warmup=None, rl_price=None,
@@ -342,9 +383,54 @@ def bench_community(args):
     return homes, oat, ghi, tou
 
 
+def spawn_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this same command, one per
+    GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run sets them), wait
+    for all of them and return the first failing exit code (0 when every rank succeeded).  Called
+    before anything touches the GPU; the ranks are child processes (no exec), rank 0 prints the
+    line.  One rank failing ends the others (their own process ids)."""
+    import socket
+    import subprocess
+    backend = os.environ.get("DRAGG_BENCH_BACKEND", "nccl")
+    if backend == "nccl":
+        import torch                       # device_count() does not initialise the GPU on this image
+        n_dev = torch.cuda.device_count()
+        if n_dev < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but {n_dev} GPU(s) visible (DRAGG_BENCH_BACKEND=gloo rehearses "
+                  f"several ranks on fewer GPUs)", file=sys.stderr)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:            # the others would wait for the failed rank forever
+                    q.kill()
+        if live:
+            time.sleep(0.2)
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.cpu_only:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and not args.cpu_only:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dt, Hh = args.dt, args.horizon_hours
@@ -352,16 +438,26 @@ def main():
     n_total = args.homes
     homes, oat, ghi, tou = bench_community(args)
 
+    rl = args.workload == "rl"
+    import numpy as np
+    H_ = Hh * dt
+    off = np.random.default_rng(5).uniform(-0.02, 0.02, (max(total_steps, args.cpu_steps_per_home), 1))
+    if args.rl_price == "smooth":       # changes at every stage (test_gpu_configs.py configs[4])
+        prices = off + (-0.03 * np.cos(np.arange(H_) / 3.0))[None, :]
+    else:
+        prices = off * np.ones((1, H_))
+
     cpu = None
-    env = {"oat": oat, "ghi": ghi, "tou": tou, "start_hour_index": 0, "reward_price": [0.0]}
+    env = {"oat": oat, "ghi": ghi, "tou": tou, "start_hour_index": 0, "reward_price": [0.0],
+           "rp_steps": [list(map(float, prices[t])) for t in range(args.cpu_steps_per_home)] if rl else None}
+    cpu_args = (args.cpu_seconds, args.cpu_workers, args.cpu_home_steps, args.cpu_milp_limit, args.cpu_steps_per_home)
     if args.cpu_only:
-        out = cpu_baseline(homes, env, args.cpu_seconds, args.cpu_workers, args.cpu_home_steps, args.cpu_milp_limit)
-        out["workload"] = (f"{n_total} homes, H={Hh * dt} ({Hh} h), {60 // dt}-min steps, month {args.month}, "
-                           f"run_rbo_mpc closed loop from t = 0")
+        out = cpu_baseline(homes, env, *cpu_args)
+        out["workload"] = cpu_workload_key(n_total, Hh, dt, args.month, args.rl_price if rl else None)
         print(json.dumps(out))
         return
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(homes, env, args.cpu_seconds, args.cpu_workers, args.cpu_home_steps, args.cpu_milp_limit)
+        cpu = cpu_baseline(homes, env, *cpu_args)
 
     import torch
     from dragg_amd.aggregator import DeviceAggregator
@@ -385,7 +481,7 @@ def main():
     shard = args.shard_of > 1 and world == 1
     agg = DeviceAggregator(homes, oat, ghi, tou, 0, total_steps, reward_price=[0.0],
                            int_mode=args.int_mode, seed=12, rank=rank, world=args.shard_of if shard else world,
-                           keep_history=not args.no_history)
+                           keep_history=not args.no_history, exact=args.exact)
     if shard:
         agg.world = 1                     # one GPU: no collectives (the shard's own sums)
     stream = torch.cuda.current_stream()
@@ -396,15 +492,7 @@ def main():
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
-    rl = args.workload == "rl"
     fh = args.forecast_horizon if rl else 0
-    import numpy as np
-    H_ = Hh * dt
-    off = np.random.default_rng(5).uniform(-0.02, 0.02, (total_steps, 1))
-    if args.rl_price == "smooth":       # changes at every stage (test_gpu_configs.py configs[4])
-        prices = off + (-0.03 * np.cos(np.arange(H_) / 3.0))[None, :]
-    else:
-        prices = off * np.ones((1, H_))
 
     def action(k):
         """rl: one reward-price action (random stand-in for the host agent's choice)."""
@@ -448,6 +536,15 @@ def main():
     if world > 1:
         torch.distributed.all_reduce(counts)
     counts = counts.cpu().tolist()
+    # the homes every rank solved (strided shards: the rank's share of the community)
+    per_rank = torch.tensor([agg.batch.N], dtype=torch.int64, device="cuda" if backend == "nccl" else "cpu")
+    if world > 1:
+        got = [torch.zeros_like(per_rank) for _ in range(world)]
+        torch.distributed.all_gather(got, per_rank)
+        homes_per_rank = [int(x.item()) for x in got]
+        dist_world = torch.distributed.get_world_size()
+    else:
+        homes_per_rank, dist_world = [int(agg.batch.N)], 1
     stat_counts = {name: int(c) for name, c in zip(names, counts)}
     success = stat_counts["optimal"] / max(1, sum(stat_counts.values()))
     solves = (agg.batch.N if shard else n_total) * args.steps * (1 + fh)
@@ -478,7 +575,11 @@ def main():
                                   "draw) swapped with homes without a battery, so the run is one the "
                                   "reference completes; null = kept (--keep-crashing-homes)"},
             "config": {"workload": workload, "baseline_config": "BASELINE.json configs[4]" if rl else "BASELINE.json configs[2]",
-                       "homes_total": n_total, "homes_per_gpu": agg.batch.N, "global_batch": n_total,
+                       "homes_total": n_total, "homes_per_gpu": agg.batch.N, "homes_per_rank": homes_per_rank,
+                       "dist_world_size": dist_world, "dist_backend": backend if world > 1 else None,
+                       "timing": "max over ranks of each rank's wall time between barriers" if world > 1
+                                 else "wall time between barriers",
+                       "global_batch": n_total,
                        "horizon": H, "mix": "40/20/20/20 base/pv/battery/pv_battery",
                        "parallelism": f"homes sharded x{world}"},
             "shard_emulation": ({"shard_of": args.shard_of, "homes": agg.batch.N,
@@ -500,8 +601,9 @@ def main():
                          "algorithmic_bytes_per_step": alg_bytes,
                          "unit_note": "one step = the hot launch + the second launch of one timestep; HIP events "
                                       "on the launch stream around run_iteration"},
-            "cpu_baseline": cpu,
-            "cpu_baseline_full": committed_cpu_baseline() if (rank == 0 and world == 1) else None,
+            "cpu_baseline": (headline_cpu_baseline(committed_cpu_baseline(cpu_workload_key(n_total, Hh, dt, args.month,
+                                                                                            args.rl_price if rl else None)), cpu)
+                             if (rank == 0 and world == 1) else None),
             "status_counts": stat_counts,
             # RL: the headline counts the rollout re-solves too; the committed steps alone:
             "committed_solves_per_s": n_total * args.steps / elapsed,

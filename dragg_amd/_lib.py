@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # DRAGG_LIB: an alternative build of the same library (kernel experiments); default in-tree
 LIB_PATH = os.environ.get("DRAGG_LIB") or os.path.join(HERE, "libdragg_mi355x.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # enums (mirror include/dragg_mi355x.h)
 BASE, PV_ONLY, BATTERY_ONLY, PV_BATTERY = 0, 1, 2, 3
@@ -80,9 +80,13 @@ class Explicit(ctypes.Structure):
                 ("draw", c_dp), ("oat", c_dp), ("ghi", c_dp), ("price", c_dp)]
 
 
+NLAUNCH = 4                    # DRAGG_NLAUNCH: hot, big, mid, narrow (dragg_mpc_kernel_info)
+LAUNCH_NAMES = ["hot", "big", "mid", "narrow"]
+
+
 class KernelInfo(ctypes.Structure):
-    _fields_ = [("vgprs", ctypes.c_int32 * 2), ("scratch_bytes", ctypes.c_int32 * 2), ("lds_bytes", ctypes.c_int32 * 2),
-                ("threads", ctypes.c_int32 * 2), ("blocks_per_cu", ctypes.c_int32 * 2)]
+    _fields_ = [(f, ctypes.c_int32 * NLAUNCH) for f in ("vgprs", "scratch_bytes", "lds_bytes", "threads",
+                                                         "blocks_per_cu")]
 
 
 EXPORTS = ["dragg_mpc_abi_version", "dragg_mpc_strerror", "dragg_mpc_lds_bytes", "dragg_mpc_workspace_bytes",
@@ -128,12 +132,12 @@ def load(path=LIB_PATH):
 
 def kernel_info(dims):
     """The launches' registers, spills, LDS and resident workgroups per CU on the current device
-    (dragg_mpc_kernel_info_get): [hot launch, second launch] dicts."""
+    (dragg_mpc_kernel_info_get): {launch name: dict} for the hot, big, mid and narrow launches."""
     info = KernelInfo()
     check(load().dragg_mpc_kernel_info_get(ctypes.byref(dims), ctypes.byref(info)))
-    return [{"vgprs": info.vgprs[i], "scratch_bytes_per_lane": info.scratch_bytes[i],
-             "lds_bytes": info.lds_bytes[i], "threads": info.threads[i],
-             "blocks_per_cu": info.blocks_per_cu[i]} for i in range(2)]
+    return {LAUNCH_NAMES[i]: {"vgprs": info.vgprs[i], "scratch_bytes_per_lane": info.scratch_bytes[i],
+                              "lds_bytes": info.lds_bytes[i], "threads": info.threads[i],
+                              "blocks_per_cu": info.blocks_per_cu[i]} for i in range(NLAUNCH)}
 
 
 def check(rc):

@@ -16,6 +16,7 @@ Homes are sharded by stride (rank r solves global homes r, r + world, r + 2 worl
 shard carries the community's type mix); the season-noise stream is keyed by the GLOBAL home
 index, so results do not depend on the shard layout.
 """
+import os
 import zlib
 
 import numpy as np
@@ -189,6 +190,28 @@ class DeviceAggregator:
         if self.hist is not None and st["hist"] is not None:
             self.hist[:t].copy_(st["hist"])
         self.timestep = t
+        return t
+
+    def resume(self, path):
+        """load_state(path) on every rank together (path None or absent: step 0), then agree on the
+        timestep.  A rank whose checkpoint is refused (another run's, corrupt, out of range) does not
+        raise before the collective -- the other ranks would wait in it forever -- but agrees on -1,
+        so that every rank raises together: the refused rank its own error, the others the
+        disagreement (or, when every rank refused, each its own error)."""
+        err, t = None, 0
+        if path is not None and os.path.isfile(path):
+            try:
+                t = self.load_state(path)
+            except (ValueError, KeyError, RuntimeError, OSError, EOFError) as e:
+                err, t = e, -1
+        try:
+            t = self.agree(t, "the checkpoint timestep to resume from")
+        except RuntimeError as e:
+            if err is not None:
+                raise err from e
+            raise
+        if err is not None:
+            raise err
         return t
 
     def agree(self, value, what):

@@ -3745,52 +3745,52 @@ int launch_kernel(K kern, int& attr_state, const KArgs& a, int blocks, int nt, s
 // several GPUs sets it once on each)
 constexpr int MAX_DEV = 64;
 
-// Waves per home of the hot launch.  With more homes than the GPU holds at once, one wave per home
-// (throughput: a SIMD interleaves 3 homes).  With few homes (a strong-scaling shard) every home is
-// resident anyway and the step time is the slowest home's latency: 2 or 4 waves then split each
-// DP stage's children (bit-identical results).  DRAGG_WAVES_PER_HOME=1|2|4 forces a choice
-// (diagnostic, A/B runs).
-template <bool EXPLICIT>
-int hot_waves(int N, int dev, size_t lds) {
-    const char* env = getenv("DRAGG_WAVES_PER_HOME");
-    if (env && (env[0] == '1' || env[0] == '2' || env[0] == '4') && env[1] == 0) return env[0] - '0';
-    // measured (1,250 homes, the 8-GPU shard of the bench: 0.495 / 0.53 / 0.80 ms per step at 1 / 2 /
-    // 4 waves per home): a stage's fixed latency (ranges, scans, barriers) dominates its passes at
-    // these front sizes, so extra waves only add barriers -- one wave per home unless forced
-    if (!env) return 1;
-    static int cap_dev[MAX_DEV][3] = {};                 // resident homes at 1, 2, 4 waves per home
-    if (!cap_dev[dev][0]) {
-        hipDeviceProp_t prop{};
-        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 1;
-        const void* k[3] = {(const void*)mpc_direct_kernel<EXPLICIT, DM_FRONT, 1>,
-                            (const void*)mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>,
-                            (const void*)mpc_direct_kernel<EXPLICIT, DM_FRONT, 4>};
-        for (int i = 0; i < 3; ++i) {
-            int per_cu = 0;
-            if (hipFuncSetAttribute(k[i], hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DYN_MAX) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k[i], WAVE << i, lds) != hipSuccess)
-                return 1;
-            cap_dev[dev][i] = max(1, per_cu * prop.multiProcessorCount);
-        }
-    }
-    return N <= cap_dev[dev][2] ? 4 : N <= cap_dev[dev][1] ? 2 : 1;
+// Diagnostic knobs, read once per process (not on every step): DRAGG_WAVES_PER_HOME=1|2|4 forces
+// the hot launch's waves per home (A/B runs); DRAGG_FORCE_STEP_DP=1 sends every home's chains to
+// the step-function DP (DM_NARROW).  Unset: one wave per home, the regular launch order.
+struct Knobs {
+    int waves = 1;
+    int force_steps = 0;
+};
+const Knobs& knobs() {
+    static const Knobs k = [] {
+        Knobs r;
+        const char* w = getenv("DRAGG_WAVES_PER_HOME");
+        if (w && (w[0] == '1' || w[0] == '2' || w[0] == '4') && w[1] == 0) r.waves = w[0] - '0';
+        const char* f = getenv("DRAGG_FORCE_STEP_DP");
+        r.force_steps = (f && f[0] == '1') ? 1 : 0;
+        return r;
+    }();
+    return k;
 }
 
-// blocks of the persistent mid launch: as many as the GPU holds at once at its LDS (<= MID_SLOTS_MAX)
+// Waves per home of the hot launch: one (measured at 1,250 homes, the 8-GPU shard of the bench:
+// 0.495 / 0.53 / 0.80 ms per step at 1 / 2 / 4 waves per home -- a stage's fixed latency (ranges,
+// scans, barriers) dominates its passes at these front sizes, so extra waves only add barriers);
+// DRAGG_WAVES_PER_HOME forces 2 or 4 (bit-identical results).
+int hot_waves() { return knobs().waves; }
+
+// blocks of the persistent mid launch: as many as the GPU holds at once at its LDS (<= MID_SLOTS_MAX),
+// cached per (device, LDS bytes): a batch with another horizon gets its own occupancy
 template <bool EXPLICIT>
 int mid_slots(int dev, int H, int S) {
-    static int slots_dev[MAX_DEV] = {};
-    if (!slots_dev[dev]) {
-        hipDeviceProp_t prop{};
-        int per_cu = 0;
-        const void* k = (const void*)mpc_direct_kernel<EXPLICIT, DM_MID, NW_MID>;
-        if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
-            hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DYN_MAX) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, NW_MID * WAVE, (size_t)mid_layout(H, S).bytes) != hipSuccess)
-            return SECOND_SLOTS;
-        slots_dev[dev] = max(1, min(MID_SLOTS_MAX, per_cu * prop.multiProcessorCount));
-    }
-    return slots_dev[dev];
+    constexpr int NC = 8;
+    static int cache_lds[MAX_DEV][NC] = {};
+    static int cache_slots[MAX_DEV][NC] = {};
+    const int lds = mid_layout(H, S).bytes;
+    for (int i = 0; i < NC; ++i)
+        if (cache_lds[dev][i] == lds) return cache_slots[dev][i];
+    hipDeviceProp_t prop{};
+    int per_cu = 0;
+    const void* k = (const void*)mpc_direct_kernel<EXPLICIT, DM_MID, NW_MID>;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+        hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DYN_MAX) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, NW_MID * WAVE, (size_t)lds) != hipSuccess)
+        return SECOND_SLOTS;
+    const int slots = max(1, min(MID_SLOTS_MAX, per_cu * prop.multiProcessorCount));
+    for (int i = 0; i < NC; ++i)
+        if (cache_lds[dev][i] == 0) { cache_lds[dev][i] = lds; cache_slots[dev][i] = slots; break; }
+    return slots;
 }
 
 template <bool EXPLICIT>
@@ -3812,10 +3812,9 @@ int launch(const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, nlen, blen);
     if (hipGetLastError() != hipSuccess) return DRAGG_E_HIP;
     const size_t lds = kernel_lds_bytes(&a.d);
-    const int nw = hot_waves<EXPLICIT>(N, dev, lds);
-    const char* fs = getenv("DRAGG_FORCE_STEP_DP");
+    const int nw = hot_waves();
     KArgs b = a;
-    b.force_steps = (fs && fs[0] == '1') ? 1 : 0;
+    b.force_steps = knobs().force_steps;
 
     const int rc = nw == 4 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 4>, attr[4], b, N, 4 * WAVE, lds, s)
                  : nw == 2 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>, attr[3], b, N, 2 * WAVE, lds, s)
@@ -3920,10 +3919,15 @@ int dragg_mpc_kernel_info_get(const dragg_mpc_dims* dims, dragg_mpc_kernel_info*
         return DRAGG_OK;
     };
     if (!direct_mode(dims)) return one((const void*)mpc_home_kernel<false>, 0, kernel_lds_bytes(dims), WAVE);
+    const int H = dims->horizon, S = dims->sub_steps;
     int r = one((const void*)mpc_direct_kernel<false, DM_FRONT>, 0, kernel_lds_bytes(dims), WAVE);
-    if (r) return r;
-    return one((const void*)mpc_direct_kernel<false, DM_BUCKET, NW_BIG>, 1,
-               (size_t)big_layout(dims->horizon, dims->sub_steps).bytes, NW_BIG * WAVE);
+    if (!r) r = one((const void*)mpc_direct_kernel<false, DM_BUCKET, NW_BIG>, 1, (size_t)big_layout(H, S).bytes,
+                    NW_BIG * WAVE);
+    if (!r) r = one((const void*)mpc_direct_kernel<false, DM_MID, NW_MID>, 2, (size_t)mid_layout(H, S).bytes,
+                    NW_MID * WAVE);
+    if (!r) r = one((const void*)mpc_direct_kernel<false, DM_NARROW, NT_STEPS / WAVE>, 3,
+                    (size_t)narrow_layout(H, S).bytes, NT_STEPS);
+    return r;
 }
 
 int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, double* out3, void* stream) {

@@ -123,10 +123,8 @@ class Aggregator:
         self.start_time = datetime.now()
         self._device_community()
         t0 = 0
-        if resume and os.path.isfile(self.state_path()):
-            t0 = self.dev.load_state(self.state_path())
-        if resume:
-            t0 = self.dev.agree(t0, "the checkpoint timestep to resume from")
+        if resume:                                 # every rank loads, then all agree (or all raise)
+            t0 = self.dev.resume(self.state_path())
             self.timestep = t0
         for t in range(t0, self.num_timesteps):
             noise = noise_fn(t)[:, self.dev.index] if noise_fn is not None else None

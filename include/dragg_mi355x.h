@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DRAGG_MPC_ABI_VERSION 6
+#define DRAGG_MPC_ABI_VERSION 7
 
 /* home types (aggregator.py:425, 468, 520, 555); bit 0 = pv, bit 1 = battery */
 enum dragg_home_type {
@@ -223,13 +223,15 @@ typedef struct dragg_mpc_explicit {
 /* Resources of the solver's launches as the code object and the runtime report them
    (hipFuncGetAttributes, hipOccupancyMaxActiveBlocksPerMultiprocessor on the current device):
    index 0 = the hot launch (int_mode round: DM_FRONT; relax / round_lp: the LP kernel),
-   index 1 = the second launch (int_mode round; zeros otherwise). */
+   index 1 = the big launch (DM_BUCKET), index 2 = the mid launch (DM_MID), index 3 = the
+   step-function launch (DM_NARROW); indices 1-3 are zeros outside int_mode round. */
+#define DRAGG_NLAUNCH 4
 typedef struct dragg_mpc_kernel_info {
-    int32_t vgprs[2];          /* registers per lane (hipFuncAttributes.numRegs)          */
-    int32_t scratch_bytes[2];  /* private memory per lane (spills; localSizeBytes)        */
-    int32_t lds_bytes[2];      /* dynamic LDS per workgroup at these dims                 */
-    int32_t threads[2];        /* threads per workgroup (one home per workgroup)          */
-    int32_t blocks_per_cu[2];  /* resident workgroups per CU at that LDS                  */
+    int32_t vgprs[DRAGG_NLAUNCH];          /* registers per lane (hipFuncAttributes.numRegs)   */
+    int32_t scratch_bytes[DRAGG_NLAUNCH];  /* private memory per lane (spills; localSizeBytes) */
+    int32_t lds_bytes[DRAGG_NLAUNCH];      /* dynamic LDS per workgroup at these dims          */
+    int32_t threads[DRAGG_NLAUNCH];        /* threads per workgroup (one home per workgroup)   */
+    int32_t blocks_per_cu[DRAGG_NLAUNCH];  /* resident workgroups per CU at that LDS           */
 } dragg_mpc_kernel_info;
 
 int dragg_mpc_abi_version(void);

@@ -15,7 +15,9 @@ tests/test_oracle_thermal.py checks that claim against every record HiGHS proved
 tests/test_gpu_exact.py compares the kernel's integer solutions with these numbers, so the GPU
 box needs neither the oracle run nor scipy.
 
-Usage:  python tests/golden/make_thermal_exact.py
+Usage:  python tests/golden/make_thermal_exact.py [FIXTURE ...]
+(FIXTURE: e.g. proven/c1_h24_proven -- only those fixtures are (re)computed and merged into the
+existing output; records are solved in parallel, one process per host core)
 """
 import glob
 import gzip
@@ -38,27 +40,38 @@ def si_of(r):
                        winter=r["season"] == "winter")
 
 
+def solve_record(args):
+    home, r = args
+    hc = M.home_const(home)
+    si = si_of(r)
+    chT = TH.chain_T(hc, si)
+    uniform = bool(np.all(chT["q"] >= 0) or np.all(chT["q"] <= 0))
+    T = TH.solve_chain(chT)
+    W = TH.solve_chain(TH.chain_W(hc, si, T[2])) if T is not None else None
+    th = None if W is None else dict(u_T=T[1], u_W=W[1])
+    return dict(uniform=uniform, cost_T=None if T is None else T[0], cost_W=None if W is None else W[0],
+                opt_obj=TH.exact_milp(hc, si, th))
+
+
 def main():
+    import multiprocessing as mp
     files = sorted(glob.glob(os.path.join(HERE, "*.json.gz"))) + sorted(glob.glob(os.path.join(HERE, "proven", "h48_*.json.gz")))
     out = {}
-    for path in files:
+    path = os.path.join(HERE, "proven", "thermal_exact.json.gz")
+    if sys.argv[1:]:
+        files = [os.path.join(HERE, f"{n}.json.gz") for n in sys.argv[1:]]
+        with gzip.open(path, "rt") as f:
+            out = json.load(f)
+    pool = mp.get_context("fork").Pool(os.cpu_count())
+    for path_in in files:
+        path = path_in
         with gzip.open(path, "rt") as f:
             d = json.load(f)
         name = os.path.basename(path)[:-8]
         if path.startswith(os.path.join(HERE, "proven")):
             name = "proven/" + name
         homes = {h["name"]: h for h in d["homes"]}
-        rows = []
-        for r in d["records"]:
-            hc = M.home_const(homes[r["name"]])
-            si = si_of(r)
-            chT = TH.chain_T(hc, si)
-            uniform = bool(np.all(chT["q"] >= 0) or np.all(chT["q"] <= 0))
-            T = TH.solve_chain(chT)
-            W = TH.solve_chain(TH.chain_W(hc, si, T[2])) if T is not None else None
-            th = None if W is None else dict(u_T=T[1], u_W=W[1])
-            rows.append(dict(uniform=uniform, cost_T=None if T is None else T[0], cost_W=None if W is None else W[0],
-                             opt_obj=TH.exact_milp(hc, si, th)))
+        rows = pool.map(solve_record, [(homes[r["name"]], r) for r in d["records"]], chunksize=4)
         out[name] = rows
         n_ok = sum(1 for x in rows if x["cost_W"] is not None)
         print(f"{name}: {len(rows)} records, {n_ok} with an integer schedule", flush=True)

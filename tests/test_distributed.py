@@ -239,6 +239,16 @@ def _resume_worker(rank, world, port, root, q):
         out["seed"] = "ok"
     except ValueError as e:
         out["seed"] = "refused"
+    # rank 1's checkpoint is another run's (refused) while rank 0's loads: both raise, none hangs
+    # in the collective (resume agrees on -1 for a refused checkpoint)
+    e = DeviceAggregator(homes, [0.0], [0.0], [0.0], **(kw | {"seed": 99 if rank == 1 else 0}))
+    try:
+        e.resume(path)
+        out["foreign"] = "ok"
+    except ValueError as ex:
+        out["foreign"] = "own: " + str(ex)
+    except RuntimeError as ex:
+        out["foreign"] = str(ex)
     # a crashing home on rank 1 only: both ranks raise the same KeyError together
     kw["batch_cls"] = ErrBatch
     d = DeviceAggregator(homes, [0.0], [0.0], [0.0], **kw)
@@ -266,3 +276,5 @@ def test_two_ranks_resume_disagreement_and_errors_raise_on_every_rank(tmp_path):
         assert "ranks disagree" in res[rank]["resume"] and "from 2 to 3" in res[rank]["resume"]
         assert res[rank]["seed"] == "refused"
         assert "home h3 at timestep 2" in res[rank]["err"]
+    assert res[1]["foreign"].startswith("own: ") and "another run" in res[1]["foreign"]
+    assert "ranks disagree" in res[0]["foreign"]
