@@ -43,9 +43,15 @@ constexpr int NTB_HOT = 64;           // key / cost buckets per stage of the hot
                                       //   (small fronts: a one-bucket-per-lane scan; measured 128: +6 % time)
 constexpr int NTB = 192;              // ... of the second launch's regular front DP and round_lp
 constexpr int NTB_BIG = 256;          // ... of the big exact pass (fronts up to NF_BIG)
-constexpr int NT_STEPS = 512;            // threads of a DM_NARROW block (8 waves: 256 VGPRs, no spills)
-constexpr int STEP_CAP = 16384;          // breakpoints per value function
-constexpr int NARROW_SLOTS = 8;          // blocks of the persistent DM_NARROW launch
+constexpr int NT_STEPS = 512;            // threads of a DM_NARROW block (8 waves)
+constexpr int NARROW_SLOTS = 16;         // blocks of the persistent DM_NARROW launch
+// the exact step-function DP (dp_steps, DM_NARROW)
+constexpr int NP_CAP = 32768;             // breakpoints of one V_k
+constexpr int POOL_CAP = 1 << 20;         // breakpoints of all V_k of one chain (the pool)
+constexpr int STEP_MAXU = 16;             // duty values 0..S (S <= 15)
+constexpr int MC_CAP = 8 * NP_CAP;        // merged candidate points of one stage ((S + 1) np, S <= 7)
+constexpr int STEP_CH = 8;                // breakpoints of one list per merge work item
+constexpr int LW_ROWS = 256;              // rows of the LP bounds L_k / W_k per slot (H < LW_ROWS)
 constexpr int NF_MID = 384;              // front capacity of the mid launch (DM_MID)
 constexpr int NTB_MID = 128;             // ... and its key / cost buckets per stage
 constexpr int MID_SLOTS_MAX = 2048;      // blocks of the persistent mid launch (~7 per CU at H = 48)
@@ -1196,6 +1202,8 @@ struct KArgs {
     const double* noise;
     int t;
     int force_steps;       // diagnostic (DRAGG_FORCE_STEP_DP=1): every home to the exact step DP
+    int pred;              // DM_NARROW: 1 = the launch of the predicted narrow homes (side stream)
+    const int* pflag;      // DM_FRONT: [N] 1 = a predicted narrow home, solved by the side launch (or NULL)
 };
 
 // --------------------------------------------------------------------------------------
@@ -1452,13 +1460,13 @@ __host__ __device__ inline size_t big_region_offset(int N, int H) {
 __host__ __device__ inline size_t big_region_bytes(int H) { return (size_t)SECOND_SLOTS * H * NF_BIG * sizeof(uint16_t); }
 // then the list of homes the second launch hands to DM_NARROW ([N] i32 + its length) and
 // (256-aligned) DM_NARROW's step-function storage, one region per block of that launch
-__host__ __device__ inline size_t step_slot_bytes(int H) {
-    // V_k breakpoints and values [H + 1][STEP_CAP] f64 each, merged candidates and interval values
-    // [(16)(STEP_CAP + 1)] f64 each (S <= 15), then the merged candidates' origins [16 (STEP_CAP + 1)]
-    // i32 and the pairwise rank tables [16 x 15][STEP_CAP + 1] i32
-    return ((size_t)2 * (H + 1) * STEP_CAP + (size_t)2 * 16 * (STEP_CAP + 1)) * sizeof(double) +
-           (size_t)(16 + 16 * 15) * (STEP_CAP + 1) * sizeof(int);
+__host__ __device__ inline size_t step_slot_bytes() {
+    // the V_k pool (breakpoints, values) [POOL_CAP] f64 each, a stage's merge keys [MC_CAP] f64 x 2 and
+    // point ids [MC_CAP] i32 x 2 past the LDS capacity (dp_steps)
+    return ((size_t)2 * POOL_CAP + (size_t)2 * MC_CAP) * sizeof(double) + (size_t)2 * MC_CAP * sizeof(int) +
+           (size_t)2 * LW_ROWS * 64 * 2 * sizeof(double);
 }
+__host__ __device__ inline int narrow_slots(int N) { return N < NARROW_SLOTS ? N : NARROW_SLOTS; }
 __host__ __device__ inline size_t narrow_list_offset(int N, int H) {
     return (big_region_offset(N, H) + big_region_bytes(H) + 255) / 256 * 256;
 }
@@ -1468,13 +1476,21 @@ __host__ __device__ inline size_t narrow_region_offset(int N, int H) {
 // then the list of homes the mid launch hands to the big one ([N] i32 + length) and (256-aligned)
 // the mid launch's back-pointer rows [MID_SLOTS_MAX][H][NF_MID] u16
 __host__ __device__ inline size_t mid_list_offset(int N, int H) {
-    return (narrow_region_offset(N, H) + (size_t)NARROW_SLOTS * step_slot_bytes(H) + 255) / 256 * 256;
+    return (narrow_region_offset(N, H) + (size_t)2 * narrow_slots(N) * step_slot_bytes() + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t mid_region_offset(int N, int H) {
     return (mid_list_offset(N, H) + (size_t)(N + 2) * sizeof(int) + 255) / 256 * 256;
 }
+// then (256-aligned) the list of the homes predicted narrow ([N] i32 + length + take counter) and
+// their flags [N] i32 (predict_kernel -> the side DM_NARROW launch; the hot launch skips them)
+__host__ __device__ inline size_t pred_list_offset(int N, int H) {
+    return (mid_region_offset(N, H) + (size_t)MID_SLOTS_MAX * H * NF_MID * sizeof(uint16_t) + 255) / 256 * 256;
+}
+__host__ __device__ inline size_t pred_flag_offset(int N, int H) {
+    return (pred_list_offset(N, H) + (size_t)(N + 2) * sizeof(int) + 255) / 256 * 256;
+}
 __host__ __device__ inline size_t direct_workspace_bytes(int N, int H) {
-    return mid_region_offset(N, H) + (size_t)MID_SLOTS_MAX * H * NF_MID * sizeof(uint16_t);
+    return pred_flag_offset(N, H) + (size_t)N * sizeof(int);
 }
 
 struct DirectLayout {
@@ -1568,18 +1584,32 @@ __host__ __device__ inline DirectLayout direct_layout(int H, int S) {
 
 __host__ __device__ inline int direct_lds_bytes(int H, int S) { return direct_layout(H, S).bytes; }
 
-// DM_NARROW: the direct layout, then the step DP's LDS: counts [H + 1] i32, scan scratch, the
-// reachable hull [2][H + 1] f64
-struct NarrowLayout { int cnt, red, rl, rh, bs, bytes; };
+// DM_NARROW: the direct layout, then the step DP's LDS (StepBufs): offsets / counts / W-row points
+// [H + 1] i32, scan scratch, list ranges, the reachable hull and the cut domains [H + 1] f64, the
+// recovery's duty values, L_k's table, then a pool with the rest of the CU's LDS: per stage V_{k+1}
+// (B, V) and the merge buffers (keys f64 x 2, ids i32 x 2) where they fit
+struct NarrowLayout { int off, cnt, wc, lc, red, xr, rng, rl, rh, dlo, dhi, xv, lt, sp, spb, bytes; };
 __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
     NarrowLayout o{};
     int p = direct_layout(H, S).bytes;
     auto take = [&](int bytes, int align) { p = (p + align - 1) / align * align; const int r = p; p += bytes; return r; };
+    o.off = take(4 * (H + 1), 4);
     o.cnt = take(4 * (H + 1), 4);
+    o.wc = take(4 * (H + 1), 4);
+    o.lc = take(4 * (H + 1), 4);
     o.red = take(4 * (NT_STEPS / 64 + 2), 4);
+    o.xr = take(4 * (NT_STEPS / 64) * STEP_MAXU, 4);
+    o.rng = take(4 * (3 * STEP_MAXU + 8), 4);
     o.rl = take(8 * (H + 1), 8);
     o.rh = take(8 * (H + 1), 8);
-    o.bs = take(8 * STEP_CAP, 16);
+    o.dlo = take(8 * (H + 1), 8);
+    o.dhi = take(8 * (H + 1), 8);
+    o.xv = take(8 * STEP_MAXU, 8);
+    o.lt = take(8 * (3 * WAVE + 2), 16);
+    // the pool takes what is left of the CU's LDS (>= the waves' PL tables of lp_domains)
+    o.sp = take(0, 16);
+    o.spb = max(NT_STEPS / 64 * 6 * WAVE * 8, ((160 * 1024 - 256) - o.sp - 64) / 64 * 64);
+    p = o.sp + o.spb;
     o.bytes = (p + 15) / 16 * 16;
     return o;
 }
@@ -3068,23 +3098,36 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
 // EXACT thermal chain DP without any dominance assumption: backward step functions (dp_steps).
 //
 // The front DP's dominance needs every feasible set F_k at least one duty step wide (and prices
-// of one sign); a tank whose feasible window narrows below one duty step (a large draw ahead)
-// breaks it (measured: the bucketed approximation then misses the optimum by up to 8.5 %).  This
-// DP assumes nothing: V_k(x) = min_u q_k u + V_{k+1}(A_k x + C_k + g u) is piecewise CONSTANT in
-// x, carried backward as sorted breakpoints and values (+inf where no schedule exists), the
-// reference's MILP optimum recovered forward by evaluating V_{k+1} at the exact successor
-// states -- the algorithm of the CPU oracle (oracle/thermal.py), restricted to the states the
-// chain can reach from x_0 (a forward interval hull).  Such V_k can hold thousands of breakpoints
-// (up to ~9k measured on narrow tanks), so it runs on a 1,024-thread block of its own launch
-// (DM_NARROW): per stage the (S+1) shifted breakpoint lists are merged by rank (binary searches),
-// each elementary interval's value taken at its midpoint, and equal neighbours compacted by block
-// scans; the V_k live in the workspace.  Returns 1 solved, 0 no integer schedule, -3 a V_k past
-// STEP_CAP breakpoints (the caller keeps its bucketed schedule).
+// of one sign).  A tank whose feasible window narrows below one duty step (a large draw ahead: the
+// tank must be nearly full when it starts) breaks it: the states from which that window can be hit
+// form a comb of period ~ one duty step, and the cost-to-go is not monotone on it (measured: the
+// Pareto fronts then miss the optimum by up to 30 %, the bucketed approximation by up to 8.5 %).
+// This DP assumes nothing: V_k(x) = min_u q_k u + V_{k+1}(A_k x + C_k + g u) is piecewise CONSTANT
+// in x, carried backward as sorted breakpoints and values (+inf where no schedule exists), the
+// MILP optimum recovered forward by evaluating V_{k+1} at the exact successor states (lowest duty
+// on ties) -- the algorithm of the CPU oracle (oracle/thermal.py).
+//
+// Only the states that can lie on an optimal path are needed: with U >= the optimum (the cost of
+// a schedule the caller holds, or of the feasibility pass's schedule), the domain of V_k is cut to
+// D_k = {x : L_k(x) + W_k(x) <= U}, L_k the LP cost-to-reach of x_k from x_0 and W_k the LP
+// cost-to-go (duties continuous: both convex piecewise linear lower bounds, lp_domains), an
+// interval that holds every optimal state.  The cut DP's value is >= the true V_k everywhere and
+// equal along every optimal path, so the recovered schedule is the uncut DP's (the same lowest-duty
+// rule picks among the same optimal continuations); measured on the bench's narrow tanks: 3-15x
+// fewer breakpoints (oracle prototype, same optimum and schedule on every case).
+//
+// One block of NT threads (DM_NARROW).  Per stage: V_{k+1} staged in LDS; the (S+1) preimage
+// lists P_u(i) = (B_i - g u - C) / A of its breakpoints merged in the total order (P, u, i) by
+// per-chunk binary searches and monotone walks (no rank tables), each merged point writing the
+// value of the elementary interval it starts (min over the duties of q u + V_{k+1} on the interval
+// of list u holding it); then zero-width intervals dropped and equal neighbours merged (two block
+// scans) into the next V_k of a pool in the workspace.  Returns 1 solved (X written), 0 no integer
+// schedule, -3 past the pool / stage capacity, -6 the cut domains lost the schedule (U below the
+// optimum: rounding; the caller retries uncut).
 // --------------------------------------------------------------------------------------
 
-
-// exclusive prefix sum over the NT threads of the block (red: >= NT/64 + 1 ints of LDS); also
-// returns the total in *tot
+// block scans for NT = 64 * waves threads (red: >= NT / 64 + 1 ints of LDS); a barrier on both
+// sides, so consecutive calls may share `red`
 template <int NT>
 DEV int block_excl_scan(int v, int* red, int tid, int* tot) {
     const int lane = tid & (WAVE - 1), w = tid / WAVE;
@@ -3100,34 +3143,227 @@ DEV int block_excl_scan(int v, int* red, int tid, int* tot) {
         all += r;
     }
     *tot = all;
+    __syncthreads();
     return off + inc - v;
+}
+template <int NT>
+DEV int block_excl_max(int v, int* red, int tid) {      // max over the threads before this one (-1: none)
+    const int lane = tid & (WAVE - 1), w = tid / WAVE;
+    const int inc = dpp_iscan(v, lane, -1, [](int a, int b) { return max(a, b); });
+    int ex = __shfl_up(inc, 1);
+    if (lane == 0) ex = -1;
+    __syncthreads();
+    if (lane == WAVE - 1) red[w] = inc;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NT / WAVE; ++i) ex = max(ex, i < w ? red[i] : -1);
+    __syncthreads();
+    return ex;
 }
 
 struct StepBufs {
-    double* VB;                  // [H + 1][STEP_CAP] breakpoints of V_k
-    double* VV;                  // [H + 1][STEP_CAP] values of V_k on [B_i, B_{i+1})
-    double* cand;                // [(S + 1)(STEP_CAP + 1)] merged candidate points
-    double* ival;                // [(S + 1)(STEP_CAP + 1) + 1] elementary-interval values
-    int* cnt;                    // LDS [H + 1] breakpoints of V_k (m + 1 points, m values)
-    int* red;                    // LDS [NT / 64 + 1] scan scratch
-    double* rl;                  // LDS [H + 1] reachable hull of x_k (widened)
-    double* rh;
-    int* corig;                  // [(S + 1)(STEP_CAP + 1)] origin (u np + i) of each merged point
-    int* rk;                     // [(S + 1) S][STEP_CAP + 1] ranks: points of list u2 before point i of list u
-    double* bs;                  // LDS [STEP_CAP]: the breakpoints of V_{k+1} while V_k is built
+    double *PB, *PV;              // global [POOL_CAP]: breakpoints / values of V_k, stage after stage
+    double *GKA, *GKB;            // global [MC_CAP]: a stage's merge keys (ping-pong) past the LDS pool
+    int *GIA, *GIB;               // global [MC_CAP]: ... and point ids (u << 24 | i)
+    double2 *Lrow, *Wrow;         // global [LW_ROWS][WAVE] (x, v): the LP rows L_k / W_k (lp_domains)
+    int *off, *cnt, *wc, *lc;     // LDS [H + 1]: pool offset of V_k, its values m (m + 1 breakpoints),
+                                  //   points of the W row / L row of x_k (lp_domains)
+    int *red;                     // LDS [NT / 64 + 2] scan scratch
+    int *xr;                      // LDS [NT / 64][STEP_MAXU] vector-scan scratch
+    int *rng;                     // LDS [3 STEP_MAXU + 8]: per-list index ranges of a stage
+    double *rl, *rh;              // LDS [H + 1] reachable hull of x_k (widened)
+    double *dlo, *dhi;            // LDS [H + 1] the LP sublevel domain of x_k (-inf / +inf: uncut)
+    double *xv;                   // LDS [STEP_MAXU] recovery: value of each duty
+    double *lt;                   // LDS [3][WAVE] + 2: L_k as a table (points, values, slopes), its
+                                  //   minimiser and minimum (the cost pruning)
+    char* sp;                     // LDS pool [spb] bytes: per stage V_{k+1} (B, V) and the merge buffers
+    int spb;                      //   (lp_domains: the waves' PL tables)
 };
+
+// exclusive prefix sums over the NT threads of the block of v[0..n) (n <= STEP_MAXU), in place
+// (xr: >= NT / 64 * STEP_MAXU ints of LDS); barriers on both sides
+template <int NT>
+DEV void block_excl_scan_vec(int* v, int n, int* xr, int tid) {
+    const int lane = tid & (WAVE - 1), w = tid / WAVE;
+    int inc[STEP_MAXU];
+#pragma unroll
+    for (int j = 0; j < STEP_MAXU; ++j) inc[j] = j < n ? dpp_iscan(v[j], lane, 0, [](int a, int b) { return a + b; }) : 0;
+    __syncthreads();
+    if (lane == WAVE - 1)
+#pragma unroll
+        for (int j = 0; j < STEP_MAXU; ++j) if (j < n) xr[w * STEP_MAXU + j] = inc[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < STEP_MAXU; ++j) {
+        if (j >= n) continue;
+        int off = 0;
+        for (int i = 0; i < w; ++i) off += xr[i * STEP_MAXU + j];
+        v[j] = off + inc[j] - v[j];
+    }
+    __syncthreads();
+}
+
+// a PL function of m <= 64 points (one per lane, ascending) into an LDS table: points, values,
+// slopes to the next point (0 past the last)
+DEV void pl_to_lds(double* T, int lane, double x, double v, int m) {
+    const double nx = __shfl_down(x, 1), nv = __shfl_down(v, 1);
+    const double s = (lane < m - 1 && nx > x) ? (nv - v) * rcp_nr(nx - x) : 0.0;
+    T[lane] = lane < m ? x : INFINITY;
+    T[WAVE + lane] = lane < m ? v : INFINITY;
+    T[2 * WAVE + lane] = s;
+}
+// value at x of the table's function, +inf outside [x_0, x_{m-1}]
+DEV double pl_tab(const double* T, int m, double x) {
+    if (m < 1 || !(x >= T[0] && x <= T[m - 1])) return INFINITY;
+    int i = 0;
+    for (int st = w_st0(m); st > 0; st >>= 1)
+        if (i + st < m && T[i + st] <= x) i += st;
+    return fma(x - T[i], T[2 * WAVE + i], T[WAVE + i]);
+}
+
+// The LP bounds of one chain (duties continuous in [0, S]) and the cut domains D_k:
+//   W_j (cost-to-go of x_j, backward from W_H = 0 on the box; make_bound's construction) on wave 1,
+//   L_k (cost-to-reach of x_k from x_0, forward: the inf-convolution of L_k mapped through the
+//   stage with the duty's linear cost, i.e. its slope list with the segment of slope q/g and
+//   length |g S| merged in, cut to the box) on wave 0, both as rows of <= 64 points;
+//   then every wave w takes the stages k = 1 + w, 1 + w + NW, ...: D_k = the sublevel set
+//   {L_k + W_k <= U} (convex: an interval, its ends interpolated on the segments where the sum
+//   crosses U, widened past rounding).  A row that would pass 64 points, or an empty cut, leaves
+//   the stages it covers uncut (-inf, +inf).  Every thread of the block calls it.
+template <int NT>
+DEV void lp_domains(const StepBufs& Sb, const double* cA, const double* cC, const double* cq, int H, int S, double g,
+                    double x0, double lo0, double hi0, double lo, double hi, double U, int tid) {
+    static_assert(NT >= 2 * WAVE, "two waves build the rows");
+    const int lane = tid & (WAVE - 1), wid = tid / WAVE;
+    auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
+    auto boxl = [&](int k) { const double b = k == 0 ? lo0 : lo; return b - tw(b); };   // box of x_{k+1}
+    auto boxh = [&](int k) { const double b = k == 0 ? hi0 : hi; return b + tw(b); };
+    double2* const Lrow = Sb.Lrow;
+    double2* const Wrow = Sb.Wrow;
+    int* const lcnt = Sb.lc;
+    const double zs = g * S, zlo = fmin(0.0, zs), zhi = fmax(0.0, zs);
+    for (int k = tid; k <= H; k += NT) { Sb.dlo[k] = -INFINITY; Sb.dhi[k] = INFINITY; Sb.wc[k] = 0; lcnt[k] = 0; }
+    __syncthreads();
+    // cut a PL function in lanes (nx ascending, m1 points) to [bl, bh]; false if empty
+    auto cut = [&](double& nx, double& nv, int m1, double bl, double bh, int& m) -> bool {
+        const double dl = fmax(bl, read_lane(nx, 0)), dh = fmin(bh, read_lane(nx, m1 - 1));
+        if (!(dl <= dh)) return false;
+        const double vdl = m1 >= 2 ? pl_eval(nx, nv, m1, dl) : read_lane(nv, 0);
+        const double vdh = m1 >= 2 ? pl_eval(nx, nv, m1, dh) : read_lane(nv, 0);
+        const bool in = lane < m1 && nx > dl && nx < dh;
+        const unsigned long long bal = __ballot(in);
+        const int m2 = __popcll(bal) + 2;
+        if (m2 > WAVE) return false;
+        const int first = bal ? __ffsll((long long)bal) - 1 : 0;
+        const int src = min(max(lane - 1 + first, 0), WAVE - 1);
+        const double sx_ = __shfl(nx, src), sv_ = __shfl(nv, src);
+        nx = lane == 0 ? dl : lane == m2 - 1 ? dh : lane < m2 ? sx_ : INFINITY;
+        nv = lane == 0 ? vdl : lane == m2 - 1 ? vdh : lane < m2 ? sv_ : INFINITY;
+        m = m2;
+        return true;
+    };
+    if (wid == 1) {
+        // W rows, j = H .. 1
+        double wx = lane == 0 ? boxl(H - 1) : lane == 1 ? boxh(H - 1) : INFINITY, wv = lane < 2 ? 0.0 : INFINITY;
+        int m = 2;
+        if (lane < m) Wrow[H * WAVE + lane] = make_double2(wx, wv);
+        if (lane == 0) Sb.wc[H] = m;
+        for (int j = H - 1; j >= 1; --j) {
+            const double A = cA[j], C = cC[j], q = cq[j];
+            if (!(A > 0.0) || m + 1 > WAVE) break;
+            const double cS = q * S;
+            const double cL = zs > 0.0 ? cS : 0.0, cR = zs > 0.0 ? 0.0 : cS;
+            const double F = lane < m ? fma(q * rcp_nr(g), wx, wv) : INFINITY;
+            const double Fm = dpp_reduce(F, [](double a, double b) { return fmin(a, b); });
+            const int js = __ffsll((long long)__ballot(F == Fm)) - 1;
+            const double px = __shfl_up(wx, 1), pv = __shfl_up(wv, 1);
+            const int m1 = m + 1;
+            double nx = lane <= js ? wx - zhi : px - zlo;
+            double nv = lane <= js ? wv + cL : pv + cR;
+            nx = (nx - C) * rcp_nr(A);
+            if (lane >= m1) { nx = INFINITY; nv = INFINITY; }
+            if (!cut(nx, nv, m1, boxl(j - 1), boxh(j - 1), m)) break;
+            wx = nx; wv = nv;
+            if (lane < m) Wrow[j * WAVE + lane] = make_double2(wx, wv);
+            if (lane == 0) Sb.wc[j] = m;
+        }
+    } else if (wid == 0) {
+        // L rows, k = 1 .. H (L_0: the point x_0 at cost 0)
+        double lx = lane == 0 ? x0 : INFINITY, lv = lane == 0 ? 0.0 : INFINITY;
+        int m = 1;
+        for (int k = 0; k < H; ++k) {
+            const double A = cA[k], C = cC[k], sg = cq[k] * rcp_nr(g);
+            if (!(A > 0.0) || m + 1 > WAVE) break;
+            if (lane < m) lx = fma(A, lx, C);
+            const double nx_ = __shfl_down(lx, 1), nv_ = __shfl_down(lv, 1);
+            const double w = nx_ - lx;
+            const bool seg = lane < m - 1;
+            const double sl = seg ? (w > 0.0 ? (nv_ - lv) * rcp_nr(w) : (nv_ > lv ? INFINITY : -INFINITY)) : INFINITY;
+            const int p = __popcll(__ballot(seg && sl < sg));          // segments flatter than the duty's
+            const double ux = __shfl_up(lx, 1), uv = __shfl_up(lv, 1);
+            const int m1 = m + 1;
+            double nx = lane <= p ? lx + zlo : ux + zhi;
+            double nv = lane <= p ? fma(sg, zlo, lv) : fma(sg, zhi, uv);
+            if (lane >= m1) { nx = INFINITY; nv = INFINITY; }
+            if (!cut(nx, nv, m1, boxl(k), boxh(k), m)) break;
+            lx = nx; lv = nv;
+            if (lane < m) Lrow[(k + 1) * WAVE + lane] = make_double2(lx, lv);
+            if (lane == 0) lcnt[k + 1] = m;
+        }
+    }
+    __syncthreads();
+    // the sublevel set of every stage, one wave per stage (its own two PL tables in bs)
+    double* const TL = reinterpret_cast<double*>(Sb.sp) + wid * 6 * WAVE;
+    double* const TW = TL + 3 * WAVE;
+    for (int k = 1 + wid; k <= H; k += NT / WAVE) {
+        const int ml = lcnt[k], mw = Sb.wc[k];
+        if (ml < 1 || mw < 2) continue;
+        const double2 l = lane < ml ? Lrow[k * WAVE + lane] : make_double2(INFINITY, INFINITY);
+        const double2 w = lane < mw ? Wrow[k * WAVE + lane] : make_double2(INFINITY, INFINITY);
+        pl_to_lds(TL, lane, l.x, l.y, ml);
+        pl_to_lds(TW, lane, w.x, w.y, mw);
+        wave_sync();
+        // the sum at both point sets (+inf outside either domain)
+        const double fl = lane < ml ? l.y + pl_tab(TW, mw, l.x) : INFINITY;
+        const double fw = lane < mw ? w.y + pl_tab(TL, ml, w.x) : INFINITY;
+        auto rmin = [](double a, double b) { return fmin(a, b); };
+        auto rmax = [](double a, double b) { return fmax(a, b); };
+        const double xa = dpp_reduce(fmin(fl <= U ? l.x : INFINITY, fw <= U ? w.x : INFINITY), rmin);
+        if (!(xa < INFINITY)) { wave_sync(); continue; }          // (rounding: leave the stage uncut)
+        const double xb = dpp_reduce(fmax(fl <= U && lane < ml ? l.x : -INFINITY, fw <= U && lane < mw ? w.x : -INFINITY), rmax);
+        const double xp = dpp_reduce(fmax(lane < ml && l.x < xa ? l.x : -INFINITY, lane < mw && w.x < xa ? w.x : -INFINITY), rmax);
+        const double xs = dpp_reduce(fmin(lane < ml && l.x > xb ? l.x : INFINITY, lane < mw && w.x > xb ? w.x : INFINITY), rmin);
+        auto f_at = [&](double x) {                                // the sum at one of the points
+            return dpp_reduce(fmin(lane < ml && l.x == x ? fl : INFINITY, lane < mw && w.x == x ? fw : INFINITY), rmin);
+        };
+        const double fa = f_at(xa), fb = f_at(xb), fp = f_at(xp), fs = f_at(xs);
+        double a = xa, b = xb;
+        if (fp < INFINITY && fp > fa) a = xp + (xa - xp) * ((fp - U) / (fp - fa));
+        if (fs < INFINITY && fs > fb) b = xb + (xs - xb) * ((U - fb) / (fs - fb));
+        a = fmin(a, xa); b = fmax(b, xb);
+        if (lane == 0) { Sb.dlo[k] = a - 4.0 * tw(a); Sb.dhi[k] = b + 4.0 * tw(b); }
+        wave_sync();
+    }
+    __syncthreads();
+}
 
 template <int NT>
 DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const double* cq, int H, int S, double g,
                  double x0, double lo0, double hi0, double lo, double hi, double* X, int sx, int sv, int tid,
-                 bool feas_only = false) {
+                 bool feas_only, bool cut_domains, double U = INFINITY) {
     // feas_only: every duty cost taken as 0, so V_k is 0 on the states with a feasible continuation and
     // +inf elsewhere; equal neighbours merge, so V_k is the feasible set as a union of a few intervals.
     // Its breakpoints are the finite region's ends of the full DP's (the same preimage arithmetic),
     // so the feasibility verdict is the full DP's -- at a fraction of its cost (no cost steps).
+    // cut_domains: V_k only on Sb.dlo/dhi (lp_domains); else those are ignored.  U < inf (with
+    // cut_domains): V_k is also set to +inf on every interval where L_k (lp_domains' cost-to-reach rows)
+    // plus V_k exceeds U -- no state there lies on a schedule of cost <= U.
     auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
     auto boxlo = [&](int k) { const double b = k == 0 ? lo0 : lo; return b - tw(b); };   // box of x_{k+1}
     auto boxhi = [&](int k) { const double b = k == 0 ? hi0 : hi; return b + tw(b); };
+    const int NU = S + 1;
+    const int lane = tid & (WAVE - 1), wid = tid / WAVE;
+    const int fail = cut_domains ? -6 : 0;
     // forward reachable hull R_{k+1} of x_{k+1} (interval arithmetic, widened past rounding)
     if (tid == 0) {
         double l = x0, u = x0;
@@ -3143,199 +3379,321 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
     __syncthreads();
     for (int k = 1; k <= H; ++k)
         if (!(Sb.rl[k] <= Sb.rh[k])) return 0;            // no state of stage k stays in its box
+    auto dom_lo = [&](int k) { return cut_domains ? fmax(Sb.rl[k], Sb.dlo[k]) : Sb.rl[k]; };
+    auto dom_hi = [&](int k) { return cut_domains ? fmin(Sb.rh[k], Sb.dhi[k]) : Sb.rh[k]; };
     // V_H = 0 on its domain
-    double* const VB = Sb.VB;
-    double* const VV = Sb.VV;
-    if (tid == 0) {
-        VB[(size_t)H * STEP_CAP + 0] = Sb.rl[H];
-        VB[(size_t)H * STEP_CAP + 1] = Sb.rh[H];
-        VV[(size_t)H * STEP_CAP + 0] = 0.0;
-        Sb.cnt[H] = 1;
+    {
+        const double l = dom_lo(H), u = dom_hi(H);
+        if (!(l <= u)) return fail;
+        if (tid == 0) { Sb.PB[0] = l; Sb.PB[1] = u; Sb.PV[0] = 0.0; Sb.off[H] = 0; Sb.cnt[H] = 1; }
     }
+    int top = 2;                                          // next free pool entry (every thread)
     __syncthreads();
-    const int NU = S + 1;
 #ifdef DRAGG_STEP_PROF
-    unsigned long long spa[6] = {0, 0, 0, 0, 0, 0}, spt = __builtin_amdgcn_s_memtime();
-    long long sp_np = 0, sp_max = 0;
-#define STP(i) do { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); spa[i] += n_ - spt; spt = n_; } while (0)
+    unsigned long long sp_t = __builtin_amdgcn_s_memtime();
+    auto sp_mark = [&](int slot_) {
+        const unsigned long long n_ = __builtin_amdgcn_s_memtime();
+        if (tid == 0 && !feas_only) X[slot_ * 8 + S_PAD] += (double)(n_ - sp_t);
+        sp_t = n_;
+    };
+#define SPM(i) sp_mark(i)
+#else
+#define SPM(i) do {} while (0)
 #endif
     for (int k = H - 1; k >= 1; --k) {
         const double A = cA[k], C = cC[k], q = feas_only ? 0.0 : cq[k];
         const double iA = 1.0 / A;
-        const double* B = VB + (size_t)(k + 1) * STEP_CAP;
-        const double* V = VV + (size_t)(k + 1) * STEP_CAP;
-        const int m = Sb.cnt[k + 1];                     // values; m + 1 breakpoints
-        const int np = m + 1;
-        double* const Bs = Sb.bs;
-        for (int i = tid; i < np; i += NT) Bs[i] = B[i];
-        __syncthreads();
-        // list u holds the preimages P_u(i) = (K_u(i) - C) / A of V_{k+1}'s breakpoints under duty u,
-        // with K_u(i) = B_i - g u.  The lists are merged by the keys K (one rounding each; P is a
-        // monotone function of K, so the merged P are sorted, equal neighbours giving zero-width
-        // intervals), ties broken by lower duty.
-        auto key = [&](int u, int i) { return Bs[i] - g * (double)u; };
-        // (1a) pairwise ranks rk[u][u2][i] = points of list u2 before point i of list u: two pointers
-        //      over contiguous chunks of i (one binary search per chunk, then a monotone walk)
-        constexpr int CH = 33;          // odd: the lanes' chunk starts fall in different LDS banks
-        const int nch = (np + CH - 1) / CH;
-        const int npair = NU * (NU - 1);
-        for (int w = tid; w < npair * nch; w += NT) {
-            const int pr = w / nch, ch = w - pr * nch;
-            const int u = pr / (NU - 1), u2r = pr - u * (NU - 1), u2 = u2r + (u2r >= u ? 1 : 0);
-            const bool le = u2 < u;                       // lower duty first on equal keys
-            const int i0 = ch * CH, i1 = min(np, i0 + CH);
-            const double k0 = key(u, i0);
-            int a = 0, b = np;
-            while (a < b) {
-                const int c = (a + b) >> 1;
-                const double v = key(u2, c);
-                if (le ? v <= k0 : v < k0) a = c + 1; else b = c;
-            }
-            int* const row = Sb.rk + (size_t)pr * (STEP_CAP + 1);
-            for (int i = i0; i < i1; ++i) {
-                const double ki = key(u, i);
-                while (a < np && (le ? key(u2, a) <= ki : key(u2, a) < ki)) ++a;
-                row[i] = a;
-            }
+        const int m = Sb.cnt[k + 1], np = m + 1;
+        const double* const Bg = Sb.PB + Sb.off[k + 1];
+        const double* const Vg = Sb.PV + Sb.off[k + 1];
+        // the LDS pool: V_{k+1} (B, V) when it fits, then the merge buffers when they fit too
+        double* const bs = reinterpret_cast<double*>(Sb.sp);
+        double* const vs = bs + np;
+        const bool staged = 16 * np <= Sb.spb;
+        if (staged)
+            for (int i = tid; i < np; i += NT) { bs[i] = Bg[i]; if (i < m) vs[i] = Vg[i]; }
+        // the cost pruning's L_k as an LDS table (wave 0), its minimiser and minimum
+        const bool prune = U < INFINITY && Sb.lc[k] >= 1;
+        if (prune && wid == 0) {
+            const int ml = Sb.lc[k];
+            const double2 l = lane < ml ? Sb.Lrow[k * WAVE + lane] : make_double2(INFINITY, INFINITY);
+            pl_to_lds(Sb.lt, lane, l.x, l.y, ml);
+            const double lm = dpp_reduce(l.y, [](double a_, double b_) { return fmin(a_, b_); });
+            const int jm = __ffsll((long long)__ballot(lane < ml && l.y == lm)) - 1;
+            if (lane == 0) { Sb.lt[3 * WAVE] = read_lane(l.x, jm); Sb.lt[3 * WAVE + 1] = lm; }
         }
+        // the domain of x_k: its box, the reachable hull, the cut
+        const double dl = fmax(boxlo(k - 1), dom_lo(k)), dh = fmin(boxhi(k - 1), dom_hi(k));
+        if (!(dl <= dh)) return fail;
         __syncthreads();
-        auto rank_in = [&](int u, int i, int u2) -> int {   // points of list u2 before point (u, i)
-            if (u2 == u) return i;
-            const int pr = u * (NU - 1) + (u2 < u ? u2 : u2 - 1);
-            return Sb.rk[(size_t)pr * (STEP_CAP + 1) + i];
-        };
-#ifdef DRAGG_STEP_PROF
-        STP(0);
-#endif
-        // (1b) every candidate to its merged position
-        const int Mc = NU * np;
-        for (int idx = tid; idx < Mc; idx += NT) {
-            const int u = idx / np, i = idx - u * np;
-            int r = i;
-            for (int u2 = 0; u2 < NU; ++u2)
-                if (u2 != u) r += rank_in(u, i, u2);
-            Sb.cand[r] = (key(u, i) - C) * iA;
-            Sb.corig[r] = idx;
-        }
-        __syncthreads();
-#ifdef DRAGG_STEP_PROF
-        STP(1);
-#endif
-        // (2) elementary intervals of the domain D_k = box of x_k and reachable hull
-        const double dl = fmax(boxlo(k - 1), Sb.rl[k]), dh = fmin(boxhi(k - 1), Sb.rh[k]);
-        if (!(dl <= dh)) return 0;
-        int jl, jh;                                       // candidates strictly inside (dl, dh)
-        {
-            int a = 0, b = Mc;
-            while (a < b) { const int c = (a + b) >> 1; if (Sb.cand[c] <= dl) a = c + 1; else b = c; }
-            jl = a;
-            a = jl; b = Mc;
-            while (a < b) { const int c = (a + b) >> 1; if (Sb.cand[c] < dh) a = c + 1; else b = c; }
-            jh = a;
-        }
-        const int T = jh - jl + 1;                        // intervals [e_t, e_{t+1})
-        // (3) each interval's value: V_{k+1} of list u's interval holding the interval (the points
-        //     of list u up to merged position jl + t - 1), min over u; NaN marks zero width
-        for (int t = tid; t < T; t += NT) {
-            const double e0 = t == 0 ? dl : Sb.cand[jl + t - 1];
-            const double e1 = t == T - 1 ? dh : Sb.cand[jl + t];
-            double best = NAN;
-            if (e1 > e0) {
-                best = INFINITY;
-                const int pos = jl + t - 1;               // the last merged point at or below e0
-                const int o = pos >= 0 ? Sb.corig[pos] : 0;
-                const int uo = o / np, io = o - uo * np;
-                for (int u = 0; u < NU; ++u) {
-                    const int i = pos < 0 ? -1 : (u == uo ? io : rank_in(uo, io, u) - 1);
-                    if (i >= 0 && i < m) best = fmin(best, fma(q, (double)u, V[i]));
+        const int top2 = 1 << (31 - __builtin_clz((unsigned)np));   // largest power of two <= np
+        // list u holds P_u(i) = (B_i - g u - C) / A; the merged order is (P, u): a point of a lower
+        // duty first on equal P.  Per list, the points inside (dl, dh) and the last one <= dl (its
+        // interval holds dl): indices [lo_u, hi_u).  (The stage is instantiated per memory space of its
+        // arrays -- LDS or the workspace -- so that LDS accesses compile to ds_ loads.)
+        auto ranges = [&](const auto* Bk) {
+            auto P = [&](int u, int i) { return (Bk[i] - g * (double)u - C) * iA; };
+            if (tid < NU) {
+                const int u = tid;
+                int le = 0, lt = 0;                       // points <= dl, points < dh
+                for (int st = top2; st > 0; st >>= 1) {
+                    if (le + st <= np && P(u, le + st - 1) <= dl) le += st;
+                    if (lt + st <= np && P(u, lt + st - 1) < dh) lt += st;
                 }
+                const int ilo = max(0, le - 1), ihi = max(lt, ilo);
+                Sb.rng[u] = ilo;
+                Sb.rng[STEP_MAXU + u] = ihi;
+                Sb.rng[2 * STEP_MAXU + u] = (le >= 1 && ilo < ihi) ? 1 : 0;   // its first point is <= dl
             }
-            Sb.ival[t] = best;
-        }
+        };
+        if (staged) ranges(bs); else ranges(Bg);
         __syncthreads();
-#ifdef DRAGG_STEP_PROF
-        STP(2);
-#endif
-        // (4) compaction: drop zero-width intervals, then merge equal neighbours (two block scans
-        //     over contiguous per-thread chunks, so that order is kept)
-        const int per = (T + NT - 1) / NT;
-        const int t0 = min(T, tid * per), t1 = min(T, t0 + per);
-        int c1 = 0;
-        for (int t = t0; t < t1; ++t) c1 += Sb.ival[t] == Sb.ival[t] ? 1 : 0;
-        int tot1;
-        int o1 = block_excl_scan<NT>(c1, Sb.red, tid, &tot1);
-        // the nonzero-width intervals (start, value) into cand[jh + 1 ...] (cand[0 .. jh) still read:
-        // starts), via a second array region: ival holds values, cand beyond Mc is free
-        double* const ks = Sb.cand + Mc;                  // kept starts  [T] (cand has 16 (cap+1) slots)
-        double* const kv = Sb.ival + T;                   // kept values  [T]
-        for (int t = t0; t < t1; ++t) {
-            const double v = Sb.ival[t];
-            if (v == v) {
-                ks[o1] = t == 0 ? dl : Sb.cand[jl + t - 1];
-                kv[o1] = v;
-                ++o1;
+        int Mc = 0, jl = 0;
+        for (int u = 0; u < NU; ++u) {
+            Mc += Sb.rng[STEP_MAXU + u] - Sb.rng[u];
+            jl += Sb.rng[2 * STEP_MAXU + u];
+        }
+        if (Mc > MC_CAP) return -3;
+        // run offsets: list u's points at [ro(u), ro(u + 1)) of the merge buffers
+        auto ro = [&](int u) {
+            int o = 0;
+            for (int j = 0; j < u && j < NU; ++j) o += Sb.rng[STEP_MAXU + j] - Sb.rng[j];
+            return o;
+        };
+        SPM(21);
+        // The merge: the lists written as runs of (key P, id = u << 24 | i) into buffer 0, then pairs of
+        // adjacent runs merged level by level (merge path: every thread takes an equal segment of a
+        // pair's output, its start found by a co-rank binary search), then each merged point's value --
+        // the value of the elementary interval it starts: min over the lists of q u + V_{k+1} on the
+        // interval of the list's last point at or before it (running per-list counts, their chunk
+        // offsets by one block scan), pruned by L_k -- and the compaction of the intervals of [dl, dh].
+        int res = 1, tot = 0;
+        auto stage = [&](const auto* Bk, const auto* Vk, auto* K0, auto* K1, auto* I0, auto* I1) {
+            auto P = [&](int u, int i) { return (Bk[i] - g * (double)u - C) * iA; };
+            auto uof = [](int id) { return id >> 24; };
+            auto less = [&](double ka, int ia, double kb, int ib) { return ka < kb || (ka == kb && uof(ia) < uof(ib)); };
+            for (int e = tid; e < Mc; e += NT) {
+                int u = 0, o = 0;
+                for (; u < NU - 1; ++u) {
+                    const int len = Sb.rng[STEP_MAXU + u] - Sb.rng[u];
+                    if (e < o + len) break;
+                    o += len;
+                }
+                const int i = Sb.rng[u] + (e - o);
+                K0[e] = P(u, i);
+                I0[e] = (u << 24) | i;
             }
+            __syncthreads();
+            auto* Ks = K0; auto* Kd = K1; auto* Is = I0; auto* Id = I1;
+            for (int w = 1; w < NU; w *= 2) {             // runs of w lists -> runs of 2w lists
+                const int npair = (NU + 2 * w - 1) / (2 * w);
+                int nseg = 0;
+                for (int pp = 0; pp < npair; ++pp) {
+                    const int o0 = ro(pp * 2 * w), o2 = ro(min(NU, (pp + 1) * 2 * w));
+                    nseg += (o2 - o0 + STEP_CH - 1) / STEP_CH;
+                }
+                for (int it = tid; it < nseg; it += NT) {
+                    int pp = 0, r = it, o0 = 0, o1 = 0, o2 = 0;
+                    for (; pp < npair; ++pp) {
+                        o0 = ro(pp * 2 * w); o1 = ro(min(NU, pp * 2 * w + w)); o2 = ro(min(NU, (pp + 1) * 2 * w));
+                        const int ns = (o2 - o0 + STEP_CH - 1) / STEP_CH;
+                        if (r < ns) break;
+                        r -= ns;
+                    }
+                    const int la = o1 - o0, lb = o2 - o1;
+                    const int d0 = r * STEP_CH, d1 = min(d0 + STEP_CH, la + lb);
+                    // co-rank: the A points among the first d0 outputs
+                    int lo_ = max(0, d0 - lb), hi_ = min(d0, la);
+                    while (lo_ < hi_) {
+                        const int mid = (lo_ + hi_) >> 1;
+                        if (less(Ks[o1 + d0 - mid - 1], Is[o1 + d0 - mid - 1], Ks[o0 + mid], Is[o0 + mid])) hi_ = mid;
+                        else lo_ = mid + 1;
+                    }
+                    int ia_ = lo_, ib_ = d0 - lo_;
+                    double ka = ia_ < la ? Ks[o0 + ia_] : INFINITY, kb = ib_ < lb ? Ks[o1 + ib_] : INFINITY;
+                    int xa = ia_ < la ? Is[o0 + ia_] : 0, xb = ib_ < lb ? Is[o1 + ib_] : 0;
+                    for (int d = d0; d < d1; ++d) {
+                        const bool ta = ib_ >= lb || (ia_ < la && less(ka, xa, kb, xb));
+                        Kd[o0 + d] = ta ? ka : kb;
+                        Id[o0 + d] = ta ? xa : xb;
+                        if (ta) {
+                            ++ia_;
+                            if (ia_ < la) { ka = Ks[o0 + ia_]; xa = Is[o0 + ia_]; }
+                        } else {
+                            ++ib_;
+                            if (ib_ < lb) { kb = Ks[o1 + ib_]; xb = Is[o1 + ib_]; }
+                        }
+                    }
+                }
+                __syncthreads();
+                auto* tk = Ks; Ks = Kd; Kd = tk;
+                auto* ti = Is; Is = Id; Id = ti;
+            }
+            // values: Ks / Is hold the merged points; Kd (free) receives each one's interval value
+            const int per = (Mc + NT - 1) / NT;
+            const int p0 = min(Mc, tid * per), p1 = min(Mc, p0 + per);
+            int cnt[STEP_MAXU];
+#pragma unroll
+            for (int j = 0; j < STEP_MAXU; ++j) cnt[j] = 0;
+            for (int p = p0; p < p1; ++p) {
+                const int u = uof(Is[p]);
+#pragma unroll
+                for (int j = 0; j < STEP_MAXU; ++j) cnt[j] += (j == u) ? 1 : 0;
+            }
+            block_excl_scan_vec<NT>(cnt, NU, Sb.xr, tid);     // points of each list before the chunk
+            double cur[STEP_MAXU];
+#pragma unroll
+            for (int j = 0; j < STEP_MAXU; ++j) {
+                const int idx = Sb.rng[j] + cnt[j] - 1;   // (j < NU: rng is defined)
+                cur[j] = (j < NU && cnt[j] >= 1 && idx < m) ? fma(q, (double)j, Vk[idx]) : INFINITY;
+            }
+            // the pruning: min of the convex L_k over [a, b] is L at the clamp of its minimiser, found by a
+            // table pointer that only moves right along the chunk (+inf outside L's domain)
+            const double xm = prune ? Sb.lt[3 * WAVE] : 0.0, lmin = prune ? Sb.lt[3 * WAVE + 1] : 0.0;
+            const int ml = prune ? Sb.lc[k] : 0;
+            int jt = 0;
+            auto Lat = [&](double x) -> double {
+                if (!(x >= Sb.lt[0] && x <= Sb.lt[ml - 1])) return INFINITY;
+                while (jt + 1 < ml && Sb.lt[jt + 1] <= x) ++jt;
+                return fma(x - Sb.lt[jt], Sb.lt[2 * WAVE + jt], Sb.lt[WAVE + jt]);
+            };
+            if (prune && p0 < p1) {
+                const double x = Ks[p0];
+                for (int st = w_st0(ml); st > 0; st >>= 1)
+                    if (jt + st < ml && Sb.lt[jt + st] <= x) jt += st;
+            }
+            for (int p = p0; p < p1; ++p) {
+                const int id = Is[p], u = uof(id), i = id & 0xFFFFFF;
+                const double v = i < m ? fma(q, (double)u, Vk[i]) : INFINITY;
+                double best = INFINITY;
+#pragma unroll
+                for (int j = 0; j < STEP_MAXU; ++j) {
+                    if (j == u) cur[j] = v;
+                    best = fmin(best, cur[j]);
+                }
+                if (prune && best < INFINITY) {
+                    const double a_ = Ks[p], b_ = p + 1 < Mc ? Ks[p + 1] : dh;
+                    const double lb_ = xm < a_ ? Lat(a_) : xm > b_ ? Lat(b_) : lmin;
+                    if (best + lb_ > U) best = INFINITY;
+                }
+                Kd[p] = best;
+            }
+            __syncthreads();
+            // intervals of [dl, dh]: t = 0 starts at dl (the value of the last merged point <= dl),
+            // t >= 1 at merged point jl + t - 1; zero-width ones dropped, equal neighbours merged
+            const auto* cand = Ks;
+            const auto* ival = Kd;
+            const int T = Mc - jl + 1;
+            const int pt = (T + NT - 1) / NT;
+            const int t0 = min(T, tid * pt), t1 = min(T, t0 + pt);
+            auto start = [&](int t) { return t == 0 ? dl : t >= T ? dh : cand[jl + t - 1]; };
+            auto value = [&](int t) { return t == 0 ? (jl > 0 ? ival[jl - 1] : INFINITY) : ival[jl + t - 1]; };
+            int lastnz = -1;
+            for (int t = t0; t < t1; ++t)
+                if (start(t + 1) > start(t)) lastnz = t;
+            const int prevnz = block_excl_max<NT>(lastnz, Sb.red, tid);
+            bool have = prevnz >= 0;
+            double pv = have ? value(prevnz) : 0.0;
+            int c = 0;
+            for (int t = t0; t < t1; ++t) {
+                if (!(start(t + 1) > start(t))) continue;
+                const double v = value(t);
+                c += (!have || v != pv) ? 1 : 0;
+                have = true;
+                pv = v;
+            }
+            int o = block_excl_scan<NT>(c, Sb.red, tid, &tot);
+            if (tot == 0) { res = fail; return; }          // (a zero-width domain)
+            if (tot + 1 > NP_CAP || top + tot + 1 > POOL_CAP) { res = -3; return; }
+            double* const OB = Sb.PB + top;
+            double* const OV = Sb.PV + top;
+            have = prevnz >= 0;
+            pv = have ? value(prevnz) : 0.0;
+            for (int t = t0; t < t1; ++t) {
+                if (!(start(t + 1) > start(t))) continue;
+                const double v = value(t);
+                if (!have || v != pv) { OB[o] = start(t); OV[o] = v; ++o; }
+                have = true;
+                pv = v;
+            }
+        };
+        // merge buffers after V_{k+1} in the pool when they fit (keys f64 x 2, ids i32 x 2)
+        const bool lds_m = staged && 16 * np + 24 * Mc + 16 <= Sb.spb;
+        if (lds_m) {
+            double* const k0 = reinterpret_cast<double*>(Sb.sp + ((16 * np + 15) & ~15));
+            double* const k1 = k0 + Mc;
+            int* const i0 = reinterpret_cast<int*>(k1 + Mc);
+            stage(bs, vs, k0, k1, i0, i0 + Mc);
+        } else if (staged) {
+            stage(bs, vs, Sb.GKA, Sb.GKB, Sb.GIA, Sb.GIB);
+        } else {
+            stage(Bg, Vg, Sb.GKA, Sb.GKB, Sb.GIA, Sb.GIB);
         }
-        __syncthreads();
-        if (tot1 == 0) return 0;
-        const int per2 = (tot1 + NT - 1) / NT;
-        const int s0 = min(tot1, tid * per2), s1 = min(tot1, s0 + per2);
-        int c2 = 0;
-        for (int j = s0; j < s1; ++j) c2 += (j == 0 || kv[j] != kv[j - 1]) ? 1 : 0;
-        int tot2;
-        int o2 = block_excl_scan<NT>(c2, Sb.red, tid, &tot2);
-        if (tot2 + 1 > STEP_CAP) return -3;
-        double* const OB = VB + (size_t)k * STEP_CAP;
-        double* const OV = VV + (size_t)k * STEP_CAP;
-        for (int j = s0; j < s1; ++j)
-            if (j == 0 || kv[j] != kv[j - 1]) { OB[o2] = ks[j]; OV[o2] = kv[j]; ++o2; }
-        if (tid == 0) { OB[tot2] = dh; Sb.cnt[k] = tot2; }
-        __syncthreads();
+        if (res != 1) return res;
+        double* const OB = Sb.PB + top;
+        if (tid == 0) { OB[tot] = dh; Sb.cnt[k] = tot; Sb.off[k] = top; }
+        SPM(23);
 #ifdef DRAGG_STEP_PROF
-        STP(3);
-        sp_np += np; sp_max = max(sp_max, (long long)np);
+        if (tid == 0 && !feas_only) {
+            X[14 * 8 + S_PAD] += (double)np; X[15 * 8 + S_PAD] = fmax(X[15 * 8 + S_PAD], (double)np);
+            X[16 * 8 + S_PAD] += (16 * np > Sb.spb ? 1.0 : 0.0) + (16 * np + 24 * Mc + 16 > Sb.spb ? 1000.0 : 0.0);
+            X[18 * 8 + S_PAD] += (double)Mc;
+        }
 #endif
+        top += tot + 1;
+        __syncthreads();
     }
+#undef SPM
 #ifdef DRAGG_STEP_PROF
-    STP(4);
+    const unsigned long long rec_t0 = __builtin_amdgcn_s_memtime();
 #endif
-    // forward recovery (wave 0: duty u on lane u): the cheapest q u + V_{k+1}(x') over the
-    // duties whose successor stays in its box, lowest duty on ties (the oracle's rule)
-    bool ok = true;
-    if (tid < WAVE) {
-        const int lane = tid;
-        double x = x0;
-        for (int k = 0; k < H && ok; ++k) {
-            const double xn = fma(cA[k], x, fma(g, (double)lane, cC[k]));
+    // forward recovery: wave u evaluates duty u's successor (q u + V_{k+1}(x') by a 64-ary search of
+    // V_{k+1}'s breakpoints), the cheapest wins, lowest duty on ties (the oracle's rule)
+    double x = x0;
+    for (int k = 0; k < H; ++k) {
+        for (int u = wid; u < NU; u += NT / WAVE) {
+            const double xn = fma(cA[k], x, fma(g, (double)u, cC[k]));
+            const double qu = feas_only ? 0.0 : cq[k] * (double)u;
             double val = INFINITY;
-            if (lane <= S && xn >= boxlo(k) && xn <= boxhi(k)) {
+            if (xn >= boxlo(k) && xn <= boxhi(k)) {
                 if (k + 1 < H) {
-                    const double* B = VB + (size_t)(k + 1) * STEP_CAP;
-                    const double* V = VV + (size_t)(k + 1) * STEP_CAP;
                     const int m = Sb.cnt[k + 1];
+                    const double* const B = Sb.PB + Sb.off[k + 1];
+                    const double* const V = Sb.PV + Sb.off[k + 1];
                     if (xn >= B[0] && xn <= B[m]) {
-                        int a = 0, b = m + 1;
-                        while (a < b) { const int c = (a + b) >> 1; if (B[c] <= xn) a = c + 1; else b = c; }
-                        val = fma(feas_only ? 0.0 : cq[k], (double)lane, V[min(a - 1, m - 1)]);
+                        // the count of breakpoints <= xn: B[lo_] <= xn, the count in (lo_, lo_ + n_]
+                        int lo_ = 0, n_ = m + 1;
+                        while (n_ > WAVE) {
+                            const int st = (n_ + WAVE - 1) / WAVE;
+                            const int j = lo_ + lane * st;
+                            const int cnt_ = __popcll(__ballot(lane * st < n_ && B[j] <= xn));
+                            const int nl = lo_ + (cnt_ - 1) * st;
+                            n_ = min(st, lo_ + n_ - nl);
+                            lo_ = nl;
+                        }
+                        const int a = lo_ + __popcll(__ballot(lane < n_ && B[lo_ + min(lane, n_ - 1)] <= xn));
+                        val = fma(feas_only ? 0.0 : cq[k], (double)u, V[min(a - 1, m - 1)]);
                     }
                 } else {
-                    val = feas_only ? 0.0 : cq[k] * (double)lane;
+                    val = qu;
                 }
             }
-            const double vm = dpp_reduce(val, [](double a, double b) { return fmin(a, b); });
-            if (!(vm < INFINITY)) { ok = false; break; }
-            const int bu = __ffsll((long long)__ballot(val == vm)) - 1;
-            x = read_lane(xn, bu);
-            if (lane == 0) { X[k * 8 + sv] = (double)bu; X[k * 8 + sx] = x; }
+            if (lane == 0) Sb.xv[u] = val;
         }
-        if (lane == 0) Sb.cnt[0] = ok ? 1 : 0;
+        __syncthreads();
+        double vm = INFINITY;
+        int bu = -1;
+        for (int u = 0; u < NU; ++u)
+            if (Sb.xv[u] < vm) { vm = Sb.xv[u]; bu = u; }
+        if (bu < 0) return fail;                           // (uniform: no duty keeps a schedule)
+        x = fma(cA[k], x, fma(g, (double)bu, cC[k]));
+        if (tid == 0) { X[k * 8 + sv] = (double)bu; X[k * 8 + sx] = x; }
+        __syncthreads();
     }
-    __syncthreads();
 #ifdef DRAGG_STEP_PROF
-    STP(5);
-    if (tid == 0) { for (int i = 0; i < 6; ++i) X[(10 + i) * 8 + S_PAD] += (double)spa[i]; X[16 * 8 + S_PAD] += (double)sp_np; X[17 * 8 + S_PAD] = fmax(X[17 * 8 + S_PAD], (double)sp_max); }
+    if (tid == 0) X[13 * 8 + S_PAD] += (double)(__builtin_amdgcn_s_memtime() - rec_t0);
 #endif
-    return Sb.cnt[0];
+    return 1;
 }
 
 // The direct path is two launches.  DM_FRONT (the hot one, one block per home) runs the exact
@@ -3461,29 +3819,85 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
             int r = -5;                                    // reason 5: the exact DP not run (S != 6)
             double2* const wg = reinterpret_cast<double2*>(ws + w_region_offset(N, H)) + (size_t)home * (H + 1) * WAVE;
             if constexpr (MODE == DM_NARROW) {
-                // the exact step-function DP (any prices, any feasible sets); past its capacity the
-                // bucketed DP's schedule is kept (reason 6)
+                // the exact step-function DP (any prices, any feasible sets)
                 const NarrowLayout nl = narrow_layout(H, a.d.sub_steps);
                 char* const sb = reinterpret_cast<char*>(smem);
-                double* const sw = reinterpret_cast<double*>(ws + narrow_region_offset(N, H) + (size_t)slot * step_slot_bytes(H));
-                double* const sw2 = sw + (size_t)2 * (H + 1) * STEP_CAP + (size_t)32 * (STEP_CAP + 1);
-                const StepBufs SB{sw, sw + (size_t)(H + 1) * STEP_CAP, sw + (size_t)2 * (H + 1) * STEP_CAP,
-                                  sw + (size_t)2 * (H + 1) * STEP_CAP + (size_t)16 * (STEP_CAP + 1),
-                                  reinterpret_cast<int*>(sb + nl.cnt), reinterpret_cast<int*>(sb + nl.red),
+                double* const sw = reinterpret_cast<double*>(ws + narrow_region_offset(N, H) +
+                                                             (size_t)(slot + (a.pred ? narrow_slots(N) : 0)) * step_slot_bytes());
+                int* const swi = reinterpret_cast<int*>(sw + 2 * (size_t)POOL_CAP + 2 * (size_t)MC_CAP);
+                double2* const swr = reinterpret_cast<double2*>(swi + 2 * (size_t)MC_CAP);
+                const StepBufs SB{sw, sw + POOL_CAP, sw + 2 * (size_t)POOL_CAP, sw + 2 * (size_t)POOL_CAP + MC_CAP,
+                                  swi, swi + MC_CAP, swr, swr + (size_t)LW_ROWS * WAVE,
+                                  reinterpret_cast<int*>(sb + nl.off), reinterpret_cast<int*>(sb + nl.cnt),
+                                  reinterpret_cast<int*>(sb + nl.wc), reinterpret_cast<int*>(sb + nl.lc),
+                                  reinterpret_cast<int*>(sb + nl.red), reinterpret_cast<int*>(sb + nl.xr),
+                                  reinterpret_cast<int*>(sb + nl.rng),
                                   reinterpret_cast<double*>(sb + nl.rl), reinterpret_cast<double*>(sb + nl.rh),
-                                  reinterpret_cast<int*>(sw2), reinterpret_cast<int*>(sw2) + (size_t)16 * (STEP_CAP + 1),
-                                  reinterpret_cast<double*>(sb + nl.bs)};
-                // feasibility first (cheap: the feasible set as a few intervals); a chain with no
-                // integer schedule -- the usual reason a home reaches this launch -- is decided there
-                r = dp_steps<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, D.x, sx, sv, lane, true);
-                if (r == 1) r = dp_steps<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, D.x, sx, sv, lane);
-                if (r >= 0) {
-                    ok = r == 1;
-                } else {
-                    ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
-                                  : dp_thermal<0>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
-                    int_path |= (1 << chain) | (6 << (4 + 4 * chain));
+                                  reinterpret_cast<double*>(sb + nl.dlo), reinterpret_cast<double*>(sb + nl.dhi),
+                                  reinterpret_cast<double*>(sb + nl.xv), reinterpret_cast<double*>(sb + nl.lt),
+                                  sb + nl.sp, nl.spb};
+                auto steps = [&](bool feas, bool cut, double U_ = INFINITY) {
+                    return dp_steps<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, D.x, sx, sv, lane, feas, cut, U_);
+                };
+                auto sched_cost = [&]() {                  // (every wave sums all stages)
+                    double c = 0.0;
+                    for (int k = lane & (WAVE - 1); k < H; k += WAVE) c += D.cq[k] * D.x[k * 8 + sv];
+                    return dpp_sum(c);
+                };
+                // an upper bound on the chain's optimum: the bucketed schedule the mid / big launch left in the
+                // solution rows; without one the feasibility pass (all duty costs 0: the feasible set as a few
+                // intervals, microseconds) decides whether any schedule exists and gives one
+                double ub = (chain == first_chain && (eflags & BK_OK)) ? sched_cost() : INFINITY;
+#ifdef DRAGG_STEP_PROF
+                unsigned long long pt = __builtin_amdgcn_s_memtime();
+                auto pmark = [&](int slot_) {
+                    const unsigned long long n_ = __builtin_amdgcn_s_memtime();
+                    if (lane == 0) D.x[slot_ * 8 + S_PAD] += (double)(n_ - pt);
+                    pt = n_;
+                };
+                if (lane == 0) D.x[19 * 8 + S_PAD] = ub;
+#define PMARK(i) pmark(i)
+#else
+#define PMARK(i) do {} while (0)
+#endif
+                r = ub < INFINITY ? 1 : steps(true, false);
+                PMARK(10);
+                if (r == 1) {
+                    if (!(ub < INFINITY)) ub = sched_cost();
+                    double qabs = 0.0;
+                    for (int k = lane & (WAVE - 1); k < H; k += WAVE) qabs += fabs(D.cq[k]) * h.S;
+                    qabs = dpp_sum(qabs);
+                    __syncthreads();
+                    const double U = ub + TOL_P * (1.0 + fabs(ub) + qabs);
+                    lp_domains<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, U, lane);
+#ifdef DRAGG_STEP_PROF
+                    if (lane == 0) {
+                        int ncut = 0;
+                        for (int k = 1; k <= H; ++k) ncut += (SB.dlo[k] > -INFINITY) ? 1 : 0;
+                        D.x[17 * 8 + S_PAD] += 100.0 * ncut;
+                        D.x[20 * 8 + S_PAD] = ub;
+                    }
+#endif
+                    PMARK(11);
+                    r = steps(false, true, U);              // V_k on the cut domains, pruned by L_k + V_k <= U
+                    PMARK(12);
+                    if (r == -6) {                          // (rounding put the optimum outside a cut: uncut)
+#ifdef DRAGG_STEP_PROF
+                        if (lane == 0) D.x[17 * 8 + S_PAD] += 1.0;
+#endif
+                        r = steps(false, false);
+                    }
+                    if (r < 0) {
+#ifdef DRAGG_STEP_PROF
+                        if (lane == 0) D.x[17 * 8 + S_PAD] += 10.0;
+#endif
+                        // past the pool's capacity: the feasibility pass's schedule stands in (reason 6)
+                        r = steps(true, false);
+                        int_path |= (1 << chain) | (6 << (4 + 4 * chain));
+                    }
                 }
+#undef PMARK
+                ok = r == 1;
                 if (!ok) int_path |= 1 << (13 + chain);
                 continue;
             }
@@ -3515,12 +3929,6 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 ok = r == 1;
             } else if (MODE == DM_FRONT) {                 // leave the home to DM_BUCKET
                 if (lane == 0) list[atomicAdd(list + N, 1)] = home | (chain << 30);
-                return;
-            } else if ((a.d.flags & DRAGG_FLAG_EXACT) && (r == -1 || r == -2 || (r == -5 && !rl_prices))) {
-                // no dominance here (mixed-sign prices without a usable bound, a feasible set
-                // narrower than one duty step, S != 6): with DRAGG_FLAG_EXACT the exact step-function
-                // DP of DM_NARROW (slow: thousands of breakpoints); else the bucketed schedule below
-                if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30);
                 return;
             } else {
                 pf.mark(DRAGG_PH_INTEGER);
@@ -3575,14 +3983,14 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                     else if (r2 == 0 && !ok) ok = false;      // exact: no integer schedule
                     else if (r2 == 0) r2 = -4;                // bound inconsistent with the schedule: keep it
                 }
-                // the bucketed schedule stands in for the optimum (int_path reports it), but a
-                // status is always exact: where the bucketed DP found no schedule and no exact pass
-                // decided it, the step-function DP decides (with DRAGG_FLAG_EXACT: every such chain)
-                if (r2 < 0 && (!ok || (a.d.flags & DRAGG_FLAG_EXACT))) {
-                    if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30);
+                // no exact pass took the chain (a feasible set narrower than one duty step, mixed-sign
+                // prices without a usable bound, a front past the big launch's capacity, S != 6): the
+                // exact step-function DP of DM_NARROW solves it, with the bucketed schedule's cost as
+                // its bound (BK_OK) -- or, where the bucketed DP found none, decides that no schedule exists
+                if (r2 < 0) {
+                    if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30) | BK_DONE | (ok ? BK_OK : 0);
                     return;
                 }
-                if (r2 < 0) int_path |= (1 << chain) | ((-r2) << (4 + 4 * chain));   // chain bit + reason
             }
             if (!ok) int_path |= 1 << (13 + chain);        // ROUND_FAIL decided by this chain
         }
@@ -3628,7 +4036,8 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
     char* const ws = reinterpret_cast<char*>(a.p.workspace);
     const int N = a.d.n_homes, H = a.d.horizon;
     if (MODE == DM_FRONT) {
-        if ((int)blockIdx.x < N) solve_direct<EXPLICIT, MODE, NW>(a, blockIdx.x, smem, 0, 0);
+        // (a home predicted narrow is the side launch's: nothing of it is read or written here)
+        if ((int)blockIdx.x < N && !(a.pflag && a.pflag[blockIdx.x])) solve_direct<EXPLICIT, MODE, NW>(a, blockIdx.x, smem, 0, 0);
         return;
     }
     // persistent: block b solves listed home b first, then takes the next ones off a shared counter
@@ -3636,7 +4045,7 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
     // ms per action against a static stride), each with its own scratch rows in the workspace (slot
     // b); blocks past the list's length leave at once, every block reaches its end and exits
     const size_t lo = MODE == DM_MID ? defer_offset(N, H) : MODE == DM_BUCKET ? mid_list_offset(N, H)
-                                                                             : narrow_list_offset(N, H);
+                    : a.pred ? pred_list_offset(N, H) : narrow_list_offset(N, H);
     int* const list = reinterpret_cast<int*>(ws + lo);
     const int cnt = min(list[N], N);
     __shared__ int take;
@@ -3652,11 +4061,90 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
 }
 
 // the three device lists' (length, take counter) pairs to zero before a step's launches
-__global__ void reset_lists_kernel(int* a, int* b, int* c) {
+__global__ void reset_lists_kernel(int* a, int* b, int* c, int* d) {
     const int i = threadIdx.x;
     if (i < 2) a[i] = 0;
     else if (i < 4) b[i - 2] = 0;
     else if (i < 6) c[i - 4] = 0;
+    else if (i < 8 && d) d[i - 6] = 0;
+}
+
+// Which homes' chains may have a feasible set narrower than one duty step (the front DP's dominance
+// does not hold there; the exact step-function DP solves them): one thread per home, before the hot
+// launch, so that those homes are solved by a DM_NARROW launch on a side stream CONCURRENTLY with the
+// hot launch instead of after it.  The front DP's narrowness test (dp_front (b)) looks at the backward
+// hulls F_H .. F_2, which depend on the stage maps and the boxes only -- not on the initial state.  The
+// tank chain's C_k holds e T_{k+1} (the indoor-air optimum, not known yet): T_{k+1} is taken anywhere in
+// its box, the hull ends carried as intervals, and a home is flagged when the narrowest possible hull
+// is narrower than a duty step (conservative: a flagged home that is not narrow is solved exactly all
+// the same).  The indoor-air chain is tested too, with the larger of the two modes' duty steps.
+template <bool EXPLICIT>
+__global__ void predict_kernel(KArgs a, int* plist, int* pflag) {
+    const int home = blockIdx.x * blockDim.x + threadIdx.x;
+    const int N = a.d.n_homes;
+    if (home >= N) return;
+    const int H = a.d.horizon, dt = a.d.dt, S = a.d.sub_steps;
+    Home h;
+    h.H = H; h.S = S; h.dt = dt; h.winter = true;
+    load_params(h, a.p.params, N, home);
+    derive(h);
+    auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
+    // the step's draw sizes (as the prologue: mpc_calc.py:193-204) and outdoor temperatures
+    const int lag = H / dt + 1, nraw = lag * dt, base_hour = (EXPLICIT ? 0 : a.t) / dt;
+    auto rawv = [&](int idx) -> double {
+        const int hh = base_hour + idx / dt - lag;
+        const double v = (hh >= 0 && hh < a.d.n_draw_hours) ? a.p.draw_hourly[(size_t)hh * N + home] : 0.0;
+        return v / dt;
+    };
+    auto draw = [&](int i) -> double {
+        if (EXPLICIT) return a.ex.draw[(size_t)i * N + home];
+        if (i < dt) return rawv(i);
+        if (i + 1 < nraw) return ((rawv(i - 1) + rawv(i)) + rawv(i + 1)) / 3.0;
+        return (rawv(i - 1) + rawv(i)) / 2.0;
+    };
+    auto oat = [&](int i) -> double {
+        return EXPLICIT ? a.ex.oat[(size_t)i * N + home] : a.p.oat[a.p.start_index + a.t + i];
+    };
+    bool narrow = false;
+    if (H >= 2) {
+        // tank chain: x_{k+1} = A_k x_k + e T_{k+1} + c_k + f u,  T_{k+1} in [Tmin, Tmax]
+        const double g = h.f, gmin = fmin(0.0, g * S), gmax = fmax(0.0, g * S);
+        const double eTlo = h.e * (h.Tmin - tw(h.Tmin)), eThi = h.e * (h.Tmax + tw(h.Tmax));
+        const double bl = h.Twmin - tw(h.Twmin), bh = h.Twmax + tw(h.Twmax);
+        double llo = bl, lhi = bl, ulo = bh, uhi = bh;
+        for (int k = H - 1; k >= 1 && !narrow; --k) {
+            if (ulo - lhi < fabs(g)) { narrow = true; break; }
+            if (k == 1) break;                         // (F_1 is not tested: its box is the state's)
+            const double df = draw(k + 1) / h.V, rem = 1 - df, d15 = df * TAP;
+            const double A = rem + (-rem * h.iRw) * 3600 * h.inv_w;
+            const double c = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
+            if (!(A > 0.0)) break;
+            const double iA = 1.0 / A, Clo = eTlo + c, Chi = eThi + c;
+            double nllo = fmax((llo - Chi - gmax) * iA, bl), nlhi = fmax((lhi - Clo - gmax) * iA, bl);
+            double nulo = fmin((ulo - Chi - gmin) * iA, bh), nuhi = fmin((uhi - Clo - gmin) * iA, bh);
+            nllo -= 2 * tw(nllo); nlhi += 2 * tw(nlhi); nulo -= 2 * tw(nulo); nuhi += 2 * tw(nuhi);
+            llo = nllo; lhi = nlhi; ulo = nulo; uhi = nuhi;
+            if (llo > uhi) break;                      // (no schedule: decided on the regular path)
+        }
+        // indoor air: C_k = oat_{k+1} / R 3600 inv_c, in both modes (the season is drawn later)
+        const double tl = h.Tmin - tw(h.Tmin), th = h.Tmax + tw(h.Tmax);
+        for (int mode = 0; mode < 2 && !narrow; ++mode) {
+            const double gT = mode == 0 ? h.Ph * 3600 * h.inv_c : -(h.Pc * 3600 * h.inv_c);
+            const double gmn = fmin(0.0, gT * S), gmx = fmax(0.0, gT * S);
+            double l = tl, u = th;
+            for (int k = H - 1; k >= 1; --k) {
+                if (u - l < fabs(gT)) { narrow = true; break; }
+                if (k == 1) break;
+                const double C = oat(k + 1) * h.iR * 3600 * h.inv_c, iA = 1.0 / h.aT;
+                l = fmax((l - C - gmx) * iA, tl);
+                u = fmin((u - C - gmn) * iA, th);
+                l -= 2 * tw(l); u += 2 * tw(u);
+                if (l > u) break;
+            }
+        }
+    }
+    pflag[home] = narrow ? 1 : 0;
+    if (narrow) plist[atomicAdd(plist + N, 1)] = home;
 }
 
 // collect_data's three sums (aggregator.py:728-755) in one 1024-thread block: 16 waves of
@@ -3747,10 +4235,12 @@ constexpr int MAX_DEV = 64;
 
 // Diagnostic knobs, read once per process (not on every step): DRAGG_WAVES_PER_HOME=1|2|4 forces
 // the hot launch's waves per home (A/B runs); DRAGG_FORCE_STEP_DP=1 sends every home's chains to
-// the step-function DP (DM_NARROW).  Unset: one wave per home, the regular launch order.
+// the step-function DP (DM_NARROW); DRAGG_NO_PREDICT=1 turns the narrow-home prediction (and its
+// side stream) off.  Unset: one wave per home, the regular launch order with the prediction.
 struct Knobs {
     int waves = 1;
     int force_steps = 0;
+    int no_predict = 0;
 };
 const Knobs& knobs() {
     static const Knobs k = [] {
@@ -3759,6 +4249,8 @@ const Knobs& knobs() {
         if (w && (w[0] == '1' || w[0] == '2' || w[0] == '4') && w[1] == 0) r.waves = w[0] - '0';
         const char* f = getenv("DRAGG_FORCE_STEP_DP");
         r.force_steps = (f && f[0] == '1') ? 1 : 0;
+        const char* np_ = getenv("DRAGG_NO_PREDICT");
+        r.no_predict = (np_ && np_[0] == '1') ? 1 : 0;
         return r;
     }();
     return k;
@@ -3793,6 +4285,28 @@ int mid_slots(int dev, int H, int S) {
     return slots;
 }
 
+// The side stream of the predicted narrow homes (one per device, the device's highest priority, so
+// that its workgroups take their CUs before the hot launch fills them) and the two events that order
+// it after the prediction and the caller's stream after it.  Created on first use.
+struct Side {
+    hipStream_t st = nullptr;
+    hipEvent_t pred_done = nullptr, side_done = nullptr;
+    bool ok = false, tried = false;
+};
+Side& side_stream(int dev) {
+    static Side sd[MAX_DEV];
+    Side& x = sd[dev];
+    if (!x.tried) {
+        x.tried = true;
+        int lo = 0, hi = 0;
+        x.ok = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+               hipStreamCreateWithPriority(&x.st, hipStreamNonBlocking, hi) == hipSuccess &&
+               hipEventCreateWithFlags(&x.pred_done, hipEventDisableTiming) == hipSuccess &&
+               hipEventCreateWithFlags(&x.side_done, hipEventDisableTiming) == hipSuccess;
+    }
+    return x;
+}
+
 template <bool EXPLICIT>
 int launch(const KArgs& a, hipStream_t s) {
     static int attr_dev[MAX_DEV][8] = {};
@@ -3807,14 +4321,36 @@ int launch(const KArgs& a, hipStream_t s) {
     int* const len = reinterpret_cast<int*>(wsb + defer_offset(N, a.d.horizon)) + N;
     int* const nlen = reinterpret_cast<int*>(wsb + narrow_list_offset(N, a.d.horizon)) + N;
     int* const blen = reinterpret_cast<int*>(wsb + mid_list_offset(N, a.d.horizon)) + N;
-    // each list's length and the persistent launch's take counter after it, in one tiny launch
-    // (three 8-byte memsets cost three fills: ~13 us of a 0.49 ms step at 1,250 homes)
-    hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, nlen, blen);
-    if (hipGetLastError() != hipSuccess) return DRAGG_E_HIP;
-    const size_t lds = kernel_lds_bytes(&a.d);
-    const int nw = hot_waves();
+    int* const plist = reinterpret_cast<int*>(wsb + pred_list_offset(N, a.d.horizon));
+    int* const pflag = reinterpret_cast<int*>(wsb + pred_flag_offset(N, a.d.horizon));
     KArgs b = a;
     b.force_steps = knobs().force_steps;
+    // narrow homes predicted ahead (int_mode round, S = 6: where the front DP runs at all)
+    Side& sd = side_stream(dev);
+    const bool predict = sd.ok && a.d.int_mode == DRAGG_INT_ROUND && a.d.sub_steps == 6 && !b.force_steps &&
+                         !knobs().no_predict;
+    // each list's length and the persistent launch's take counter after it, in one tiny launch
+    // (three 8-byte memsets cost three fills: ~13 us of a 0.49 ms step at 1,250 homes)
+    hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, nlen, blen, predict ? plist + N : nullptr);
+    if (hipGetLastError() != hipSuccess) return DRAGG_E_HIP;
+    if (predict) {
+        hipLaunchKernelGGL(predict_kernel<EXPLICIT>, dim3((N + 255) / 256), dim3(256), 0, s, b, plist, pflag);
+        if (hipGetLastError() != hipSuccess) return DRAGG_E_HIP;
+        // the side stream: after the prediction, the step-function DP of the predicted homes (their
+        // own workspace slots), concurrently with the hot / mid / big launches on the caller's stream
+        if (hipEventRecord(sd.pred_done, s) != hipSuccess || hipStreamWaitEvent(sd.st, sd.pred_done, 0) != hipSuccess)
+            return DRAGG_E_HIP;
+        KArgs c = b;
+        c.pred = 1;
+        const int rcs = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_NARROW, NT_STEPS / WAVE>, attr[5], c,
+                                      min(N, NARROW_SLOTS), NT_STEPS, (size_t)narrow_layout(a.d.horizon, a.d.sub_steps).bytes,
+                                      sd.st);
+        if (rcs) return rcs;
+        if (hipEventRecord(sd.side_done, sd.st) != hipSuccess) return DRAGG_E_HIP;
+        b.pflag = pflag;
+    }
+    const size_t lds = kernel_lds_bytes(&a.d);
+    const int nw = hot_waves();
 
     const int rc = nw == 4 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 4>, attr[4], b, N, 4 * WAVE, lds, s)
                  : nw == 2 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>, attr[3], b, N, 2 * WAVE, lds, s)
@@ -3829,8 +4365,12 @@ int launch(const KArgs& a, hipStream_t s) {
     const int rc2 = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_BUCKET, NW_BIG>, attr[2], b, min(N, SECOND_SLOTS),
                                   NW_BIG * WAVE, (size_t)big_layout(a.d.horizon, a.d.sub_steps).bytes, s);
     if (rc2) return rc2;
-    return launch_kernel(mpc_direct_kernel<EXPLICIT, DM_NARROW, NT_STEPS / WAVE>, attr[5], b, min(N, NARROW_SLOTS),
-                         NT_STEPS, (size_t)narrow_layout(a.d.horizon, a.d.sub_steps).bytes, s);
+    const int rcn = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_NARROW, NT_STEPS / WAVE>, attr[5], b, min(N, NARROW_SLOTS),
+                                  NT_STEPS, (size_t)narrow_layout(a.d.horizon, a.d.sub_steps).bytes, s);
+    if (rcn) return rcn;
+    // the step is complete on the caller's stream only with the side stream's work
+    if (predict && hipStreamWaitEvent(s, sd.side_done, 0) != hipSuccess) return DRAGG_E_HIP;
+    return DRAGG_OK;
 }
 
 }  // namespace

@@ -135,11 +135,10 @@ typedef struct dragg_mpc_dims {
 
 /* dims.flags */
 enum dragg_flag {
-    /* int_mode round: solve every chain the Pareto-front DP cannot take (a feasible set narrower
-       than one duty step, mixed-sign prices without a usable bound, a front past 2,048 labels)
-       by the exact step-function DP too.  Without it such a chain keeps the bucketed DP's
-       schedule (reported in out.int_path) unless that finds none -- statuses are exact either
-       way.  The step-function DP is slow (milliseconds per chain). */
+    /* Accepted for compatibility with ABI v6 and without effect since v7: int_mode round is exact
+       on every chain by default -- a chain the Pareto-front DPs cannot take (a feasible set
+       narrower than one duty step, mixed-sign prices without a usable bound, a front past 2,048
+       labels, S != 6) is solved by the exact step-function DP (out.int_path bit 15). */
     DRAGG_FLAG_EXACT = 1
 };
 
@@ -176,13 +175,10 @@ typedef struct dragg_mpc_out {
     int64_t* cycles;            /* optional [DRAGG_NPHASE][N] shader cycles per phase   */
     int32_t* int_path;          /* optional [N] integer-DP path (int_mode round): 0 = the
                                    exact front DP solved both thermal chains; bit 0 / bit 1
-                                   = the indoor-air / tank chain used the bucketed
-                                   approximation; bits 4-7 / 8-11 its reason: 1 mixed-sign
-                                   prices, 2 a feasible set narrower than one duty step,
-                                   3 front overflow, 4 the exact pass's bound contradicts
-                                   the bucketed schedule, 5 the exact DP was not run
-                                   (S != 6), 6 the exact step-function DP past its
-                                   capacity; bit 12 = solved by a later launch (its front
+                                   = the indoor-air / tank chain kept an approximate (feasible)
+                                   schedule; bits 4-7 / 8-11 its reason -- since v7 only
+                                   6: the exact step-function DP past its capacity (its pool
+                                   of 2^20 breakpoints per chain; never measured); bit 12 = solved by a later launch (its front
                                    outgrew the hot launch's capacity; still exact when
                                    bits 0-11 are 0); bits 13 / 14 = status ROUND_FAIL
                                    decided by the indoor-air / tank chain (no integer duty

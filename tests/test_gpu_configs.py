@@ -256,9 +256,9 @@ def test_config4_rl_10k_homes_price_broadcast_and_rollouts(gpu):
           f"exact fronts under the smooth RL price), {n_off} of them left the exact DP (front overflow past "
           f"NF_BIG); sampled fallback gaps to the exact optimum: {len(fb)}, mean "
           f"{fb.mean() if len(fb) else 0:.1e}, max {fb.max() if len(fb) else 0:.1e}")
-    # exactness under RL prices: at most 0.1 % of the homes may outgrow the big fronts (measured:
-    # 0 of 10,000 here, 3 of 80,000 over 8 RL steps, tools/count_paths.py)
-    assert n_off <= 0.001 * int((st == 0).sum()), n_off
+    # exactness under RL prices: a chain past the big fronts goes to the step-function DP (round 3
+    # allowed 0.1 % of the homes an approximate schedule; now none)
+    assert n_off == 0, n_off
     _report("configs[4] RL 10k homes, H = 48, July, rollout = commit", agg, homes, [(t,) + res], min_opt=0)
 
 
@@ -289,18 +289,32 @@ def bench_day(gpu):
     agg = DeviceAggregator(homes, oat, ghi, tou, 0, steps, reward_price=[0.0], seed=12, keep_history=False)
     b = agg.batch
     kept = []
+    n_approx = n_steps_dp = 0
     for t in range(steps):
         prev = (b.vals.clone(), b.fc.clone())
         agg.run_iteration()
         st = b.status.cpu().numpy()
         path = b.int_path.cpu().numpy()
+        n_approx += int(((path & L.PATH_APPROX_MASK) != 0).sum())
+        n_steps_dp += int(((path & L.PATH_STEPS) != 0).sum())
         if not ((st == L.ST_ROUND_FAIL).any() or _narrow(path).any()):
             continue
         kept.append(dict(t=t, prev_vals=prev[0].cpu().numpy(), prev_fc=prev[1].cpu().numpy(),
                          noise=b.season_noise(t).cpu().numpy(), status=st, obj=b.obj.cpu().numpy(),
                          vals=b.vals.cpu().numpy(), fc=b.fc.cpu().numpy(), path=path))
     torch.cuda.synchronize()
-    return dict(homes=homes, oat=oat, ghi=ghi, tou=tou, steps=kept, n_steps=steps)
+    return dict(homes=homes, oat=oat, ghi=ghi, tou=tou, steps=kept, n_steps=steps, n_approx=n_approx,
+                n_steps_dp=n_steps_dp)
+
+
+def test_bench_default_build_exact_on_every_solve(bench_day):
+    """The default build over 100 bench steps (10,000 homes, H = 48, July: 1,000,000 solves): no solve
+    keeps an approximate integer schedule (int_path bits 0-11 clear on every home and step) -- every
+    chain the Pareto-front DPs cannot take is solved by the exact step-function DP (bit 15)."""
+    d = bench_day
+    print(f"bench workload, {d['n_steps']} steps: {d['n_steps_dp']} home-steps through the step-function DP, "
+          f"{d['n_approx']} on an approximate schedule")
+    assert d["n_approx"] == 0
 
 
 def test_bench_round_fail_solves_have_no_integer_schedule(bench_day):
@@ -335,13 +349,12 @@ def test_bench_round_fail_solves_have_no_integer_schedule(bench_day):
 
 def test_bench_narrow_set_solves_gap_bound_and_exact_mode(bench_day):
     """A chain whose feasible set is narrower than one duty step somewhere in the horizon breaks the
-    front DP's dominance.  By default such a chain keeps the bucketed DP's schedule (int_path reason
-    2) -- its status is exact all the same: where the bucketed DP finds no schedule the exact
-    step-function DP decides (test_round_fail_status_matches_the_joint_model).  Every such solve of
-    the bench workload over 100 steps: status identical to the exact optimum (oracle/thermal.py
-    exact_milp, the assumption-free backward DP), never below it, gap bounded (measured max 8.5 %).
-    With DRAGG_FLAG_EXACT (MPCBatch exact=True) the same steps take the step-function DP: every one
-    equals the exact optimum (1e-6) and none keeps an approximation."""
+    front DP's dominance; the exact step-function DP (DM_NARROW, int_path bit 15) solves it, on the
+    domains cut by the LP bounds and the bucketed schedule's cost.  Every such solve of the bench
+    workload over 100 steps: status and objective equal to the exact optimum (oracle/thermal.py
+    exact_milp, the assumption-free backward DP; 1e-9).  MPCBatch(exact=True) (DRAGG_FLAG_EXACT, kept for
+    the ABI, no effect) gives the same: every one equals the exact optimum and none keeps an
+    approximation."""
     import torch
     from dragg_amd import _lib as L
     from dragg_amd.aggregator import DeviceAggregator
@@ -389,4 +402,4 @@ def test_bench_narrow_set_solves_gap_bound_and_exact_mode(bench_day):
     print(f"exact mode: {n_exact} of those solves by the step-function DP, all at the exact optimum")
 
 
-NARROW_GAP_BOUND = 0.10      # the bucketed approximation's measured worst case (8.5 %, home 7519 at t = 60)
+NARROW_GAP_BOUND = 1e-9      # exact: the step-function DP (round 3's bucketed approximation: 8.5 %, home 7519 at t = 60)

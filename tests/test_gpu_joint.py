@@ -85,11 +85,11 @@ def test_round_fail_status_matches_the_joint_model(gpu):
 
 
 def test_narrow_set_solves_against_the_joint_optimum(gpu):
-    """Narrow-set cases: with DRAGG_FLAG_EXACT the kernel's objective equals the exact sequential
-    optimum (oracle/thermal.py's assumption-free step-function DP + the LP, 1e-9 rel), never lies
-    below HiGHS's dual bound on the joint model, and equals HiGHS's joint optimum where it proved one
-    (1e-6).  The default build (bucketed schedule on these chains) is reported and bounded: never
-    below the optimum, the same status."""
+    """Narrow-set cases: the kernel's objective equals the exact sequential optimum (oracle/thermal.py's
+    assumption-free step-function DP + the LP, 1e-9 rel), never lies below HiGHS's dual bound on the
+    joint model, and equals HiGHS's joint optimum where it proved one (1e-6).  The default build takes
+    these chains to the step-function DP too (DRAGG_FLAG_EXACT is kept for ABI compatibility and changes
+    nothing): the same status, the same objective (1e-9), no chain left on an approximate schedule."""
     from dragg_amd import _lib as L
     cases = [c for c in _cases() if c["status"] != "round_fail"]
     if not cases:
@@ -115,9 +115,9 @@ def test_narrow_set_solves_against_the_joint_optimum(gpu):
             assert abs(g) <= 1e-6, (where, obj, c["joint_opt"])
             gaps.append(g)
         dg = (dflt[j][1] - obj) / max(1.0, abs(obj))
-        assert dg >= -1e-9, (where, dflt[j][1], obj)          # the bucketed schedule is never below
+        assert abs(dg) <= 1e-9, (where, dflt[j][1], obj)      # the default build is exact as well
+        assert not (dflt[j][2] & L.PATH_APPROX_MASK), (where, dflt[j][2])
         dgaps.append(dg)
     d = np.array(dgaps)
     print(f"narrow-set cases: {len(cases)}; exact mode = the sequential optimum on all, = HiGHS's proven joint "
-          f"optimum on {n_proven}; default build's bucketed schedules: max gap {d.max() if len(d) else 0:.2e}, "
-          f"{int((d > 1e-9).sum())} above 1e-9")
+          f"optimum on {n_proven}; default build: max |gap| to it {np.abs(d).max() if len(d) else 0:.2e}")

@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-r04}
 mkdir -p $OUT
-TESTS=${TESTS:-"tests/test_gpu_step.py tests/test_gpu_edges.py tests/test_gpu_replay_proven.py"}
+TESTS=${TESTS:-tests}
 if [ "$TESTS" != "none" ]; then
   timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v -s --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest.log; exit 1; }
   tail -2 $OUT/pytest.log
@@ -14,7 +14,7 @@ fi
 run() { name=$1; shift; timeout -k 10 400 python3 bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "$name failed"; tail -5 $OUT/$name.err; exit 1; }
   python3 -c "
 import json; d=json.load(open('$OUT/$name.json')); print('$name', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],4), 'ms/step', 'n_gpus', d['n_gpus'], d['config'].get('homes_per_rank'), {k: v for k, v in d['status_counts'].items() if v and k != 'optimal'})"; }
-for spec in ${LINES:-driver full96 exact96 shard8 gloo2}; do
+for spec in ${LINES:-driver full96 shard8 gloo2}; do
   case $spec in
     driver) run driver --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 ;;
     full96) run full96 --steps 96 --warmup 4 --cpu-seconds 0 ;;
