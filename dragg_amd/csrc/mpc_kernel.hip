@@ -1080,10 +1080,10 @@ DEV double objective(const Home& h, const Lds& L, int lane, int nt = WAVE, doubl
 
 struct Io {
     double* vals;          // [NVAL][N]
-    double* fc;            // [NFC][H][N]
+    double* fc;            // [N][NFC][H] (home-contiguous)
     int N, home;
     __device__ double& v(int key) const { return vals[(size_t)key * N + home]; }
-    __device__ double& f(int key, int j, int H) const { return fc[((size_t)key * H + j) * N + home]; }
+    __device__ double& f(int key, int j, int H) const { return fc[((size_t)home * DRAGG_NFC + key) * H + j]; }
 };
 
 // success branch of cleanup_and_finish (mpc_calc.py:486-526)
@@ -1597,9 +1597,9 @@ __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
     o.cnt = take(4 * (H + 1), 4);
     o.wc = take(4 * (H + 1), 4);
     o.lc = take(4 * (H + 1), 4);
-    o.red = take(4 * (NT_STEPS / 64 + 2), 4);
+    o.red = take(4 * 32, 4);
     o.xr = take(4 * (NT_STEPS / 64) * STEP_MAXU, 4);
-    o.rng = take(4 * (3 * STEP_MAXU + 8), 4);
+    o.rng = take(4 * (4 * STEP_MAXU + 8), 4);
     o.rl = take(8 * (H + 1), 8);
     o.rh = take(8 * (H + 1), 8);
     o.dlo = take(8 * (H + 1), 8);
@@ -3146,6 +3146,35 @@ DEV int block_excl_scan(int v, int* red, int tid, int* tot) {
     __syncthreads();
     return off + inc - v;
 }
+// ... with one barrier: the caller keeps `red` (>= NT / 64 ints) for this call alone until a later barrier
+template <int NT>
+DEV int block_excl_scan1(int v, int* red, int tid, int* tot) {
+    const int lane = tid & (WAVE - 1), w = tid / WAVE;
+    const int inc = dpp_iscan(v, lane, 0, [](int a, int b) { return a + b; });
+    if (lane == WAVE - 1) red[w] = inc;
+    __syncthreads();
+    int off = 0, all = 0;
+#pragma unroll
+    for (int i = 0; i < NT / WAVE; ++i) {
+        const int r = red[i];
+        off += i < w ? r : 0;
+        all += r;
+    }
+    *tot = all;
+    return off + inc - v;
+}
+template <int NT>
+DEV int block_excl_max1(int v, int* red, int tid) {     // max over the threads before this one (-1: none)
+    const int lane = tid & (WAVE - 1), w = tid / WAVE;
+    const int inc = dpp_iscan(v, lane, -1, [](int a, int b) { return max(a, b); });
+    int ex = __shfl_up(inc, 1);
+    if (lane == 0) ex = -1;
+    if (lane == WAVE - 1) red[w] = inc;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NT / WAVE; ++i) ex = max(ex, i < w ? red[i] : -1);
+    return ex;
+}
 template <int NT>
 DEV int block_excl_max(int v, int* red, int tid) {      // max over the threads before this one (-1: none)
     const int lane = tid & (WAVE - 1), w = tid / WAVE;
@@ -3168,9 +3197,9 @@ struct StepBufs {
     double2 *Lrow, *Wrow;         // global [LW_ROWS][WAVE] (x, v): the LP rows L_k / W_k (lp_domains)
     int *off, *cnt, *wc, *lc;     // LDS [H + 1]: pool offset of V_k, its values m (m + 1 breakpoints),
                                   //   points of the W row / L row of x_k (lp_domains)
-    int *red;                     // LDS [NT / 64 + 2] scan scratch
+    int *red;                     // LDS [32] scan scratch (two scans of a stage: [0, 16), [16, 32))
     int *xr;                      // LDS [NT / 64][STEP_MAXU] vector-scan scratch
-    int *rng;                     // LDS [3 STEP_MAXU + 8]: per-list index ranges of a stage
+    int *rng;                     // LDS [4 STEP_MAXU + 8]: per-list index ranges of a stage, run offsets
     double *rl, *rh;              // LDS [H + 1] reachable hull of x_k (widened)
     double *dlo, *dhi;            // LDS [H + 1] the LP sublevel domain of x_k (-inf / +inf: uncut)
     double *xv;                   // LDS [STEP_MAXU] recovery: value of each duty
@@ -3181,14 +3210,13 @@ struct StepBufs {
 };
 
 // exclusive prefix sums over the NT threads of the block of v[0..n) (n <= STEP_MAXU), in place
-// (xr: >= NT / 64 * STEP_MAXU ints of LDS); barriers on both sides
+// (xr: >= NT / 64 * STEP_MAXU ints of LDS, the caller's alone until a later barrier); one barrier
 template <int NT>
 DEV void block_excl_scan_vec(int* v, int n, int* xr, int tid) {
     const int lane = tid & (WAVE - 1), w = tid / WAVE;
     int inc[STEP_MAXU];
 #pragma unroll
     for (int j = 0; j < STEP_MAXU; ++j) inc[j] = j < n ? dpp_iscan(v[j], lane, 0, [](int a, int b) { return a + b; }) : 0;
-    __syncthreads();
     if (lane == WAVE - 1)
 #pragma unroll
         for (int j = 0; j < STEP_MAXU; ++j) if (j < n) xr[w * STEP_MAXU + j] = inc[j];
@@ -3200,7 +3228,6 @@ DEV void block_excl_scan_vec(int* v, int n, int* xr, int tid) {
         for (int i = 0; i < w; ++i) off += xr[i * STEP_MAXU + j];
         v[j] = off + inc[j] - v[j];
     }
-    __syncthreads();
 }
 
 // a PL function of m <= 64 points (one per lane, ascending) into an LDS table: points, values,
@@ -3408,10 +3435,9 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         const double* const Vg = Sb.PV + Sb.off[k + 1];
         // the LDS pool: V_{k+1} (B, V) when it fits, then the merge buffers when they fit too
         double* const bs = reinterpret_cast<double*>(Sb.sp);
-        double* const vs = bs + np;
-        const bool staged = 16 * np <= Sb.spb;
+        const bool staged = 8 * np <= Sb.spb;
         if (staged)
-            for (int i = tid; i < np; i += NT) { bs[i] = Bg[i]; if (i < m) vs[i] = Vg[i]; }
+            for (int i = tid; i < np; i += NT) bs[i] = Bg[i];
         // the cost pruning's L_k as an LDS table (wave 0), its minimiser and minimum
         const bool prune = U < INFINITY && Sb.lc[k] >= 1;
         if (prune && wid == 0) {
@@ -3448,6 +3474,12 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         };
         if (staged) ranges(bs); else ranges(Bg);
         __syncthreads();
+        if (tid == 0) {                                   // run offsets ro(u) = points of the lists before u
+            int o = 0;
+            for (int u = 0; u < NU; ++u) { Sb.rng[3 * STEP_MAXU + u] = o; o += Sb.rng[STEP_MAXU + u] - Sb.rng[u]; }
+            for (int u = NU; u <= STEP_MAXU; ++u) Sb.rng[3 * STEP_MAXU + u] = o;
+        }
+        __syncthreads();
         int Mc = 0, jl = 0;
         for (int u = 0; u < NU; ++u) {
             Mc += Sb.rng[STEP_MAXU + u] - Sb.rng[u];
@@ -3455,11 +3487,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         }
         if (Mc > MC_CAP) return -3;
         // run offsets: list u's points at [ro(u), ro(u + 1)) of the merge buffers
-        auto ro = [&](int u) {
-            int o = 0;
-            for (int j = 0; j < u && j < NU; ++j) o += Sb.rng[STEP_MAXU + j] - Sb.rng[j];
-            return o;
-        };
+        auto ro = [&](int u) { return Sb.rng[3 * STEP_MAXU + min(u, STEP_MAXU)]; };
         SPM(21);
         // The merge: the lists written as runs of (key P, id = u << 24 | i) into buffer 0, then pairs of
         // adjacent runs merged level by level (merge path: every thread takes an equal segment of a
@@ -3468,23 +3496,19 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         // interval of the list's last point at or before it (running per-list counts, their chunk
         // offsets by one block scan), pruned by L_k -- and the compaction of the intervals of [dl, dh].
         int res = 1, tot = 0;
-        auto stage = [&](const auto* Bk, const auto* Vk, auto* K0, auto* K1, auto* I0, auto* I1) {
+        auto stage = [&](const auto* Bk, const auto* Vk, auto* I0, auto* I1, auto* VAL) {
             auto P = [&](int u, int i) { return (Bk[i] - g * (double)u - C) * iA; };
             auto uof = [](int id) { return id >> 24; };
+            auto key = [&](int id) { return P(uof(id), id & 0xFFFFFF); };
+            // a before b in the merged order (P, u); the caller passes keys it already holds
             auto less = [&](double ka, int ia, double kb, int ib) { return ka < kb || (ka == kb && uof(ia) < uof(ib)); };
             for (int e = tid; e < Mc; e += NT) {
-                int u = 0, o = 0;
-                for (; u < NU - 1; ++u) {
-                    const int len = Sb.rng[STEP_MAXU + u] - Sb.rng[u];
-                    if (e < o + len) break;
-                    o += len;
-                }
-                const int i = Sb.rng[u] + (e - o);
-                K0[e] = P(u, i);
-                I0[e] = (u << 24) | i;
+                int u = 0;
+                while (u < NU - 1 && e >= ro(u + 1)) ++u;
+                I0[e] = (u << 24) | (Sb.rng[u] + (e - ro(u)));
             }
             __syncthreads();
-            auto* Ks = K0; auto* Kd = K1; auto* Is = I0; auto* Id = I1;
+            auto* Is = I0; auto* Id = I1;
             for (int w = 1; w < NU; w *= 2) {             // runs of w lists -> runs of 2w lists
                 const int npair = (NU + 2 * w - 1) / (2 * w);
                 int nseg = 0;
@@ -3506,30 +3530,30 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
                     int lo_ = max(0, d0 - lb), hi_ = min(d0, la);
                     while (lo_ < hi_) {
                         const int mid = (lo_ + hi_) >> 1;
-                        if (less(Ks[o1 + d0 - mid - 1], Is[o1 + d0 - mid - 1], Ks[o0 + mid], Is[o0 + mid])) hi_ = mid;
+                        const int ib = Is[o1 + d0 - mid - 1], ia = Is[o0 + mid];
+                        if (less(key(ib), ib, key(ia), ia)) hi_ = mid;
                         else lo_ = mid + 1;
                     }
                     int ia_ = lo_, ib_ = d0 - lo_;
-                    double ka = ia_ < la ? Ks[o0 + ia_] : INFINITY, kb = ib_ < lb ? Ks[o1 + ib_] : INFINITY;
                     int xa = ia_ < la ? Is[o0 + ia_] : 0, xb = ib_ < lb ? Is[o1 + ib_] : 0;
+                    double ka = ia_ < la ? key(xa) : INFINITY, kb = ib_ < lb ? key(xb) : INFINITY;
                     for (int d = d0; d < d1; ++d) {
                         const bool ta = ib_ >= lb || (ia_ < la && less(ka, xa, kb, xb));
-                        Kd[o0 + d] = ta ? ka : kb;
                         Id[o0 + d] = ta ? xa : xb;
                         if (ta) {
                             ++ia_;
-                            if (ia_ < la) { ka = Ks[o0 + ia_]; xa = Is[o0 + ia_]; }
+                            if (ia_ < la) { xa = Is[o0 + ia_]; ka = key(xa); }
                         } else {
                             ++ib_;
-                            if (ib_ < lb) { kb = Ks[o1 + ib_]; xb = Is[o1 + ib_]; }
+                            if (ib_ < lb) { xb = Is[o1 + ib_]; kb = key(xb); }
                         }
                     }
                 }
                 __syncthreads();
-                auto* tk = Ks; Ks = Kd; Kd = tk;
                 auto* ti = Is; Is = Id; Id = ti;
             }
-            // values: Ks / Is hold the merged points; Kd (free) receives each one's interval value
+            SPM(25);
+            // values: Is holds the merged points; VAL receives each one's interval value
             const int per = (Mc + NT - 1) / NT;
             const int p0 = min(Mc, tid * per), p1 = min(Mc, p0 + per);
             int cnt[STEP_MAXU];
@@ -3547,21 +3571,6 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
                 const int idx = Sb.rng[j] + cnt[j] - 1;   // (j < NU: rng is defined)
                 cur[j] = (j < NU && cnt[j] >= 1 && idx < m) ? fma(q, (double)j, Vk[idx]) : INFINITY;
             }
-            // the pruning: min of the convex L_k over [a, b] is L at the clamp of its minimiser, found by a
-            // table pointer that only moves right along the chunk (+inf outside L's domain)
-            const double xm = prune ? Sb.lt[3 * WAVE] : 0.0, lmin = prune ? Sb.lt[3 * WAVE + 1] : 0.0;
-            const int ml = prune ? Sb.lc[k] : 0;
-            int jt = 0;
-            auto Lat = [&](double x) -> double {
-                if (!(x >= Sb.lt[0] && x <= Sb.lt[ml - 1])) return INFINITY;
-                while (jt + 1 < ml && Sb.lt[jt + 1] <= x) ++jt;
-                return fma(x - Sb.lt[jt], Sb.lt[2 * WAVE + jt], Sb.lt[WAVE + jt]);
-            };
-            if (prune && p0 < p1) {
-                const double x = Ks[p0];
-                for (int st = w_st0(ml); st > 0; st >>= 1)
-                    if (jt + st < ml && Sb.lt[jt + st] <= x) jt += st;
-            }
             for (int p = p0; p < p1; ++p) {
                 const int id = Is[p], u = uof(id), i = id & 0xFFFFFF;
                 const double v = i < m ? fma(q, (double)u, Vk[i]) : INFINITY;
@@ -3571,63 +3580,101 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
                     if (j == u) cur[j] = v;
                     best = fmin(best, cur[j]);
                 }
-                if (prune && best < INFINITY) {
-                    const double a_ = Ks[p], b_ = p + 1 < Mc ? Ks[p + 1] : dh;
-                    const double lb_ = xm < a_ ? Lat(a_) : xm > b_ ? Lat(b_) : lmin;
-                    if (best + lb_ > U) best = INFINITY;
-                }
-                Kd[p] = best;
+                VAL[p] = best;
             }
             __syncthreads();
+            SPM(26);
             // intervals of [dl, dh]: t = 0 starts at dl (the value of the last merged point <= dl),
-            // t >= 1 at merged point jl + t - 1; zero-width ones dropped, equal neighbours merged
-            const auto* cand = Ks;
-            const auto* ival = Kd;
+            // t >= 1 at merged point jl + t - 1; zero-width ones dropped, the L_k + V_k > U pruning
+            // applied, equal neighbours merged
             const int T = Mc - jl + 1;
             const int pt = (T + NT - 1) / NT;
             const int t0 = min(T, tid * pt), t1 = min(T, t0 + pt);
-            auto start = [&](int t) { return t == 0 ? dl : t >= T ? dh : cand[jl + t - 1]; };
-            auto value = [&](int t) { return t == 0 ? (jl > 0 ? ival[jl - 1] : INFINITY) : ival[jl + t - 1]; };
+            auto start = [&](int t) { return t == 0 ? dl : t >= T ? dh : key(Is[jl + t - 1]); };
+            auto raw = [&](int t) { return t == 0 ? (jl > 0 ? VAL[jl - 1] : INFINITY) : VAL[jl + t - 1]; };
+            // the pruning: min of the convex L_k over [a, b] is L at the clamp of its minimiser (+inf outside
+            // its domain), by a table pointer that only moves right along the chunk
+            const double xm = prune ? Sb.lt[3 * WAVE] : 0.0, lmin = prune ? Sb.lt[3 * WAVE + 1] : 0.0;
+            const int ml = prune ? Sb.lc[k] : 0;
+            int jt = 0;
+            auto Lat = [&](double x) -> double {
+                if (!(x >= Sb.lt[0] && x <= Sb.lt[ml - 1])) return INFINITY;
+                while (jt + 1 < ml && Sb.lt[jt + 1] <= x) ++jt;
+                return fma(x - Sb.lt[jt], Sb.lt[2 * WAVE + jt], Sb.lt[WAVE + jt]);
+            };
+            auto Lseek = [&](double x) {
+                jt = 0;
+                for (int st = w_st0(ml); st > 0; st >>= 1)
+                    if (jt + st < ml && Sb.lt[jt + st] <= x) jt += st;
+            };
+            auto value = [&](int t, double a_, double b_) {
+                double v = raw(t);
+                if (prune && v < INFINITY) {
+                    const double lb_ = xm < a_ ? Lat(a_) : xm > b_ ? Lat(b_) : lmin;
+                    if (v + lb_ > U) v = INFINITY;
+                }
+                return v;
+            };
             int lastnz = -1;
-            for (int t = t0; t < t1; ++t)
-                if (start(t + 1) > start(t)) lastnz = t;
-            const int prevnz = block_excl_max<NT>(lastnz, Sb.red, tid);
-            bool have = prevnz >= 0;
-            double pv = have ? value(prevnz) : 0.0;
-            int c = 0;
-            for (int t = t0; t < t1; ++t) {
-                if (!(start(t + 1) > start(t))) continue;
-                const double v = value(t);
-                c += (!have || v != pv) ? 1 : 0;
-                have = true;
-                pv = v;
+            {
+                double s0 = start(t0);
+                for (int t = t0; t < t1; ++t) {
+                    const double s1 = start(t + 1);
+                    if (s1 > s0) lastnz = t;
+                    s0 = s1;
+                }
             }
-            int o = block_excl_scan<NT>(c, Sb.red, tid, &tot);
+            const int prevnz = block_excl_max1<NT>(lastnz, Sb.red, tid);
+            double pv0 = 0.0;                              // the previous nonzero interval's (pruned) value
+            if (prevnz >= 0) {
+                const double a_ = start(prevnz), b_ = start(prevnz + 1);
+                if (prune) Lseek(a_);
+                pv0 = value(prevnz, a_, b_);
+            }
+            auto walk = [&](auto&& emit) {                 // the chunk's kept intervals, in order
+                bool have = prevnz >= 0;
+                double pv = pv0;
+                double s0 = start(t0);
+                if (prune) Lseek(s0);
+                for (int t = t0; t < t1; ++t) {
+                    const double s1 = start(t + 1);
+                    if (s1 > s0) {
+                        const double v = value(t, s0, s1);
+                        if (!have || v != pv) emit(s0, v);
+                        have = true;
+                        pv = v;
+                    }
+                    s0 = s1;
+                }
+            };
+            int c = 0;
+            walk([&](double, double) { ++c; });
+            int o = block_excl_scan1<NT>(c, Sb.red + 16, tid, &tot);
             if (tot == 0) { res = fail; return; }          // (a zero-width domain)
             if (tot + 1 > NP_CAP || top + tot + 1 > POOL_CAP) { res = -3; return; }
             double* const OB = Sb.PB + top;
             double* const OV = Sb.PV + top;
-            have = prevnz >= 0;
-            pv = have ? value(prevnz) : 0.0;
-            for (int t = t0; t < t1; ++t) {
-                if (!(start(t + 1) > start(t))) continue;
-                const double v = value(t);
-                if (!have || v != pv) { OB[o] = start(t); OV[o] = v; ++o; }
-                have = true;
-                pv = v;
-            }
+            walk([&](double s_, double v_) { OB[o] = s_; OV[o] = v_; ++o; });
         };
-        // merge buffers after V_{k+1} in the pool when they fit (keys f64 x 2, ids i32 x 2)
-        const bool lds_m = staged && 16 * np + 24 * Mc + 16 <= Sb.spb;
+        // the pool: V_{k+1}'s breakpoints (and values when they fit too), then the merge buffers when
+        // they fit as well (ids i32 x 2, values f64)
+        const bool lds_v = staged && 16 * np + 32 <= Sb.spb;
+        const bool lds_m = staged && 8 * (lds_v ? 2 : 1) * np + 16 * Mc + 48 <= Sb.spb;
+        if (lds_v) {
+            double* const vs = bs + np;
+            for (int i = tid; i < m; i += NT) vs[i] = Vg[i];
+        }
+        SPM(24);
         if (lds_m) {
-            double* const k0 = reinterpret_cast<double*>(Sb.sp + ((16 * np + 15) & ~15));
-            double* const k1 = k0 + Mc;
-            int* const i0 = reinterpret_cast<int*>(k1 + Mc);
-            stage(bs, vs, k0, k1, i0, i0 + Mc);
+            const int ob = (8 * (lds_v ? 2 : 1) * np + 15) & ~15, oi = (ob + 8 * Mc + 15) & ~15;
+            double* const vl = reinterpret_cast<double*>(Sb.sp + ob);
+            int* const i0 = reinterpret_cast<int*>(Sb.sp + oi);
+            if (lds_v) stage(bs, bs + np, i0, i0 + Mc, vl);
+            else stage(bs, Vg, i0, i0 + Mc, vl);
         } else if (staged) {
-            stage(bs, vs, Sb.GKA, Sb.GKB, Sb.GIA, Sb.GIB);
+            stage(bs, Vg, Sb.GIA, Sb.GIB, Sb.GKA);
         } else {
-            stage(Bg, Vg, Sb.GKA, Sb.GKB, Sb.GIA, Sb.GIB);
+            stage(Bg, Vg, Sb.GIA, Sb.GIB, Sb.GKA);
         }
         if (res != 1) return res;
         double* const OB = Sb.PB + top;
@@ -3636,7 +3683,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
 #ifdef DRAGG_STEP_PROF
         if (tid == 0 && !feas_only) {
             X[14 * 8 + S_PAD] += (double)np; X[15 * 8 + S_PAD] = fmax(X[15 * 8 + S_PAD], (double)np);
-            X[16 * 8 + S_PAD] += (16 * np > Sb.spb ? 1.0 : 0.0) + (16 * np + 24 * Mc + 16 > Sb.spb ? 1000.0 : 0.0);
+            X[16 * 8 + S_PAD] += (8 * np > Sb.spb ? 1.0 : 0.0) + (8 * np + 16 * Mc + 48 > Sb.spb ? 1000.0 : 0.0);
             X[18 * 8 + S_PAD] += (double)Mc;
         }
 #endif
@@ -3844,10 +3891,34 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                     for (int k = lane & (WAVE - 1); k < H; k += WAVE) c += D.cq[k] * D.x[k * 8 + sv];
                     return dpp_sum(c);
                 };
+                // a predicted home (side launch) starts from chain 0, the indoor air, which is narrow in
+                // practice only where the prediction flags the wrong chain: the regular exact front DP (all
+                // waves of the block; its W table and exchange area in the pool) solves it far faster than the
+                // step-function DP (which takes it where the front DP does not apply)
+                if (a.pred && h.S == 6 && chain == 0) {
+                    double* const wl = reinterpret_cast<double*>(SB.sp);
+                    char* const xch = SB.sp + 3 * WAVE * sizeof(double);
+                    double2* const wg = reinterpret_cast<double2*>(ws + w_region_offset(N, H)) + (size_t)home * (H + 1) * WAVE;
+                    const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
+                                       wg, wl, wl + WAVE, wl + 2 * WAVE, xch};
+                    const int rf = dp_front<6, NF, NF_BOUND, NB_CAP, NTB, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv,
+                                                                        rl_prices, INFINITY, nullptr);
+                    __syncthreads();
+                    if (rf >= 0) {
+                        ok = rf == 1;
+                        if (!ok) int_path |= 1 << (13 + chain);
+                        continue;
+                    }
+                }
                 // an upper bound on the chain's optimum: the bucketed schedule the mid / big launch left in the
                 // solution rows; without one the feasibility pass (all duty costs 0: the feasible set as a few
                 // intervals, microseconds) decides whether any schedule exists and gives one
                 double ub = (chain == first_chain && (eflags & BK_OK)) ? sched_cost() : INFINITY;
+                // a predicted home has no bucketed schedule yet: the bucketed DP gives one (a bound within a
+                // few % of the optimum: far smaller cut domains than the feasibility pass's schedule)
+                if (a.pred && h.S == 6 && !(ub < INFINITY) &&
+                    dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv))
+                    ub = sched_cost();
 #ifdef DRAGG_STEP_PROF
                 unsigned long long pt = __builtin_amdgcn_s_memtime();
                 auto pmark = [&](int slot_) {
@@ -4122,13 +4193,33 @@ __global__ void predict_kernel(KArgs a, int* plist, int* pflag) {
             const double iA = 1.0 / A, Clo = eTlo + c, Chi = eThi + c;
             double nllo = fmax((llo - Chi - gmax) * iA, bl), nlhi = fmax((lhi - Clo - gmax) * iA, bl);
             double nulo = fmin((ulo - Chi - gmin) * iA, bh), nuhi = fmin((uhi - Clo - gmin) * iA, bh);
-            nllo -= 2 * tw(nllo); nlhi += 2 * tw(nlhi); nulo -= 2 * tw(nulo); nuhi += 2 * tw(nuhi);
+            nllo -= 2 * tw(nllo); nlhi -= 0.5 * tw(nlhi); nulo += 0.5 * tw(nulo); nuhi += 2 * tw(nuhi);
             llo = nllo; lhi = nlhi; ulo = nulo; uhi = nuhi;
             if (llo > uhi) break;                      // (no schedule: decided on the regular path)
         }
-        // indoor air: C_k = oat_{k+1} / R 3600 inv_c, in both modes (the season is drawn later)
+        // indoor air: C_k = oat_{k+1} / R 3600 inv_c, in the season's mode (the prologue's draw,
+        // mpc_calc.py:220-223, 303-309; a wrong-season mode is often nearly infeasible, i.e. narrow)
+        bool winter;
+        if (EXPLICIT) {
+            winter = a.ex.winter[home] != 0;
+        } else {
+#pragma clang fp contract(off)
+            const int s0 = a.p.start_index + a.t;
+            double mx = a.p.oat[s0];
+            for (int k = 0; k < H; ++k) {
+                double z;
+                if (a.noise) z = a.noise[(size_t)k * N + home];
+                else {
+                    double z0, z1;
+                    normal_pair(a.p.seed, a.p.home_offset + home * max(a.p.home_stride, 1), a.t, k >> 1, &z0, &z1);
+                    z = (k & 1) ? z1 : z0;
+                }
+                mx = fmax(mx, a.p.oat[s0 + k + 1] + pow(1.1, (double)k) * z);
+            }
+            winter = mx <= 30.0;
+        }
         const double tl = h.Tmin - tw(h.Tmin), th = h.Tmax + tw(h.Tmax);
-        for (int mode = 0; mode < 2 && !narrow; ++mode) {
+        for (int mode = winter ? 0 : 1; mode == (winter ? 0 : 1) && !narrow; ++mode) {
             const double gT = mode == 0 ? h.Ph * 3600 * h.inv_c : -(h.Pc * 3600 * h.inv_c);
             const double gmn = fmin(0.0, gT * S), gmx = fmax(0.0, gT * S);
             double l = tl, u = th;
@@ -4235,12 +4326,14 @@ constexpr int MAX_DEV = 64;
 
 // Diagnostic knobs, read once per process (not on every step): DRAGG_WAVES_PER_HOME=1|2|4 forces
 // the hot launch's waves per home (A/B runs); DRAGG_FORCE_STEP_DP=1 sends every home's chains to
-// the step-function DP (DM_NARROW); DRAGG_NO_PREDICT=1 turns the narrow-home prediction (and its
-// side stream) off.  Unset: one wave per home, the regular launch order with the prediction.
+// the step-function DP (DM_NARROW); DRAGG_PREDICT=1 turns the narrow-home prediction (and its side
+// stream) on -- measured slower at 10k homes and at the 8-way shard (the side launch's step DP outlasts
+// the hot launch; the prediction costs ~0.1 ms at 1,250 homes), so off by default.  Unset: one wave per
+// home, the regular launch order.
 struct Knobs {
     int waves = 1;
     int force_steps = 0;
-    int no_predict = 0;
+    int no_predict = 1;
 };
 const Knobs& knobs() {
     static const Knobs k = [] {
@@ -4249,8 +4342,8 @@ const Knobs& knobs() {
         if (w && (w[0] == '1' || w[0] == '2' || w[0] == '4') && w[1] == 0) r.waves = w[0] - '0';
         const char* f = getenv("DRAGG_FORCE_STEP_DP");
         r.force_steps = (f && f[0] == '1') ? 1 : 0;
-        const char* np_ = getenv("DRAGG_NO_PREDICT");
-        r.no_predict = (np_ && np_[0] == '1') ? 1 : 0;
+        const char* pr_ = getenv("DRAGG_PREDICT");
+        r.no_predict = (pr_ && pr_[0] == '1') ? 0 : 1;
         return r;
     }();
     return k;

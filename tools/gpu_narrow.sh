@@ -5,6 +5,9 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-narrow}
 mkdir -p $OUT
+( while sleep 60; do echo "tick $(date +%T)" >> $OUT/heartbeat; done ) &
+HB=$!
+trap "kill $HB" EXIT
 if [ -f varlib/stprof.so ]; then
   DRAGG_LIB=varlib/stprof.so timeout -k 10 300 python -u tools/step_prof.py --steps 50 > $OUT/step_prof.log 2>&1 || { echo STEPPROF_FAIL; tail -20 $OUT/step_prof.log; exit 1; }
   tail -2 $OUT/step_prof.log
@@ -16,9 +19,9 @@ timeout -k 10 300 python3 bench.py --steps 96 --warmup 4 --cpu-seconds 0 > $OUT/
 python3 -c "import json; d=json.load(open('$OUT/full96.json')); print('full96', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],4), 'ms/step')"
 for v in ${EXTRA:-nopred shard8}; do
   case $v in
-    nopred) DRAGG_NO_PREDICT=1 timeout -k 10 300 python3 bench.py --steps 96 --warmup 4 --cpu-seconds 0 > $OUT/$v.json 2> $OUT/$v.err || { echo BENCH_FAIL $v; tail -5 $OUT/$v.err; exit 1; } ;;
+    pred) DRAGG_PREDICT=1 timeout -k 10 300 python3 bench.py --steps 96 --warmup 4 --cpu-seconds 0 > $OUT/$v.json 2> $OUT/$v.err || { echo BENCH_FAIL $v; tail -5 $OUT/$v.err; exit 1; } ;;
     shard8) timeout -k 10 300 python3 bench.py --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 > $OUT/$v.json 2> $OUT/$v.err || { echo BENCH_FAIL $v; tail -5 $OUT/$v.err; exit 1; } ;;
-    shard8np) DRAGG_NO_PREDICT=1 timeout -k 10 300 python3 bench.py --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 > $OUT/$v.json 2> $OUT/$v.err || { echo BENCH_FAIL $v; tail -5 $OUT/$v.err; exit 1; } ;;
+    shard8p) DRAGG_PREDICT=1 timeout -k 10 300 python3 bench.py --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 > $OUT/$v.json 2> $OUT/$v.err || { echo BENCH_FAIL $v; tail -5 $OUT/$v.err; exit 1; } ;;
   esac
   python3 -c "import json; d=json.load(open('$OUT/$v.json')); print('$v', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],4), 'ms/step')"
 done

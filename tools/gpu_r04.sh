@@ -6,6 +6,9 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-r04}
 mkdir -p $OUT
+( while sleep 60; do echo "tick $(date +%T)" >> $OUT/heartbeat; done ) &
+HB=$!
+trap "kill $HB" EXIT
 TESTS=${TESTS:-tests}
 if [ "$TESTS" != "none" ]; then
   timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v -s --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest.log; exit 1; }

@@ -30,10 +30,10 @@ agg = DeviceAggregator(homes, oat, ghi, tou, 0, a.steps, reward_price=[0.0], see
 N, H = agg.batch.N, agg.batch.H
 par = ((N * H * 336 * 2 + 255) // 256) * 256
 rows = []
-names = ["feas", "lpdom", "cutpass", "recov", "sum_np", "max_np", "global", "flags", "sum_Mc", "ub_ext", "ub", "ranges", "scatter", "compact"]
+names = ["feas", "lpdom", "cutpass", "recov", "sum_np", "max_np", "global", "flags", "sum_Mc", "ub_ext", "ub", "ranges", "-", "compact", "vstage", "merge", "values"]
 for t in range(a.steps):
     ws = agg.batch.workspace.view(torch.uint8)[par:par + N * 8 * H * 8].view(torch.float64).view(N, H, 8)
-    ws[:, 10:24, 7] = 0.0
+    ws[:, 10:27, 7] = 0.0
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
     t0.record()
@@ -43,7 +43,7 @@ for t in range(a.steps):
     path = agg.batch.int_path.cpu().numpy()
     idx = np.flatnonzero(path & L.PATH_STEPS)
     if len(idx):
-        v = ws[idx][:, 10:24, 7].cpu().numpy()
+        v = ws[idx][:, 10:27, 7].cpu().numpy()
         for j, i in enumerate(idx):
             rows.append([t, int(i)] + v[j].tolist())
             print(f"t={t} home {i} step {t0.elapsed_time(t1):.3f} ms: " +
