@@ -138,7 +138,11 @@ class MPCBatch:
                              tou if tou is not None else [0.0], start_index)
         self.set_reward_price(reward_price)
         self.vals = torch.full((L.NVAL, self.N), float("nan"), dtype=torch.float64, device=dev)
-        self.fc = torch.full((L.NFC, self.H, self.N), float("nan"), dtype=torch.float64, device=dev)
+        # the forecast fields <key>_<j>: stored home-contiguous ([N][NFC][H], dragg_mi355x.h: one home's
+        # fields are one 5.7 KB run the solver writes with coalesced stores), seen here as the
+        # [NFC][H][N] view the rest of the host code indexes
+        self.fc_store = torch.full((self.N, L.NFC, self.H), float("nan"), dtype=torch.float64, device=dev)
+        self.fc = self.fc_store.permute(1, 2, 0)
         self.status = torch.zeros(self.N, dtype=torch.int32, device=dev)
         self.iters = torch.zeros(self.N, dtype=torch.int32, device=dev)
         self.obj = torch.zeros(self.N, dtype=torch.float64, device=dev)
@@ -189,7 +193,7 @@ class MPCBatch:
                          home_stride=self.home_stride)
 
     def _hash(self):
-        return L.Hash(vals=L.ptr(self.vals), fc=L.ptr(self.fc))
+        return L.Hash(vals=L.ptr(self.vals), fc=L.ptr(self.fc_store))
 
     def _out(self, hist=None):
         return L.Out(status=L.ptr(self.status), iters=L.ptr(self.iters), obj=L.ptr(self.obj),

@@ -30,7 +30,7 @@
  *    (a hipStream_t, NULL = default stream); no host synchronisation inside.
  *  - The per-home redis hash (`redis_client.py`, all values str) is replaced by
  *    two fp64 arrays: `vals` [DRAGG_NVAL][N] (the scalar fields a step writes)
- *    and `fc` [DRAGG_NFC][H][N] (the `<key>_<j>` forecast fields, rewritten only
+ *    and `fc` [N][DRAGG_NFC][H] (the `<key>_<j>` forecast fields, rewritten only
  *    by a successful solve).  NaN means "field absent from the hash".
  */
 #ifndef DRAGG_MI355X_H
@@ -71,7 +71,7 @@ enum dragg_param {
     DRAGG_NPARAM
 };
 
-/* forecast keys: rows of fc[DRAGG_NFC][H][N] (`<key>_<j>` hash fields, mpc_calc.py:514-520) */
+/* forecast keys: rows of fc[N][DRAGG_NFC][H] (`<key>_<j>` hash fields, mpc_calc.py:514-520) */
 enum dragg_fc_key {
     DRAGG_K_P_GRID = 0, DRAGG_K_FORECAST_P_GRID, DRAGG_K_P_LOAD, DRAGG_K_TEMP_IN_EV,
     DRAGG_K_TEMP_WH_EV, DRAGG_K_HVAC_COOL, DRAGG_K_HVAC_HEAT, DRAGG_K_WH_HEAT, DRAGG_K_COST,
@@ -163,7 +163,7 @@ typedef struct dragg_mpc_problem {
 
 typedef struct dragg_mpc_hash {
     double* vals;               /* [DRAGG_NVAL][N]  in/out, NaN = absent               */
-    double* fc;                 /* [DRAGG_NFC][H][N] in/out                            */
+    double* fc;                 /* [N][DRAGG_NFC][H] in/out (home-contiguous since v7) */
 } dragg_mpc_hash;
 
 typedef struct dragg_mpc_out {
