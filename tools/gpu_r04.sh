@@ -14,10 +14,11 @@ if [ "$TESTS" != "none" ]; then
   timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v -s --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest.log; exit 1; }
   tail -2 $OUT/pytest.log
 fi
-run() { name=$1; shift; timeout -k 10 400 python3 bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "$name failed"; tail -5 $OUT/$name.err; exit 1; }
+run() { name=$1; shift; timeout -k 10 400 python3 bench.py "$@" > $OUT/$name.out 2> $OUT/$name.err || { echo "$name failed"; tail -5 $OUT/$name.err; exit 1; }
+  grep '^{' $OUT/$name.out | tail -1 > $OUT/$name.json
   python3 -c "
 import json; d=json.load(open('$OUT/$name.json')); print('$name', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],4), 'ms/step', 'n_gpus', d['n_gpus'], d['config'].get('homes_per_rank'), {k: v for k, v in d['status_counts'].items() if v and k != 'optimal'})"; }
-for spec in ${LINES:-driver full96 shard8 gloo2}; do
+for spec in ${LINES:-driver full96 shard8 shard4 gloo2}; do
   case $spec in
     driver) run driver --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 ;;
     full96) run full96 --steps 96 --warmup 4 --cpu-seconds 0 ;;
