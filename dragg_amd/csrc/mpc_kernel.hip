@@ -1461,9 +1461,9 @@ __host__ __device__ inline size_t big_region_bytes(int H) { return (size_t)SECON
 // then the list of homes the second launch hands to DM_NARROW ([N] i32 + its length) and
 // (256-aligned) DM_NARROW's step-function storage, one region per block of that launch
 __host__ __device__ inline size_t step_slot_bytes() {
-    // the V_k pool (breakpoints, values) [POOL_CAP] f64 each, a stage's merge keys [MC_CAP] f64 x 2 and
-    // point ids [MC_CAP] i32 x 2 past the LDS capacity (dp_steps)
-    return ((size_t)2 * POOL_CAP + (size_t)2 * MC_CAP) * sizeof(double) + (size_t)2 * MC_CAP * sizeof(int) +
+    // the V_k pool (breakpoints, values) [POOL_CAP] f64 each and a stage's point ids [MC_CAP] i32 x 2
+    // (merge ping-pong; the free one then holds the values' codes) past the LDS capacity (dp_steps)
+    return (size_t)2 * POOL_CAP * sizeof(double) + (size_t)2 * MC_CAP * sizeof(int) +
            (size_t)2 * LW_ROWS * 64 * 2 * sizeof(double);
 }
 __host__ __device__ inline int narrow_slots(int N) { return N < NARROW_SLOTS ? N : NARROW_SLOTS; }
@@ -3192,8 +3192,7 @@ DEV int block_excl_max(int v, int* red, int tid) {      // max over the threads 
 
 struct StepBufs {
     double *PB, *PV;              // global [POOL_CAP]: breakpoints / values of V_k, stage after stage
-    double *GKA, *GKB;            // global [MC_CAP]: a stage's merge keys (ping-pong) past the LDS pool
-    int *GIA, *GIB;               // global [MC_CAP]: ... and point ids (u << 24 | i)
+    int *GIA, *GIB;               // global [MC_CAP]: a stage's point ids (u << 24 | i), ping-pong, past the LDS pool
     double2 *Lrow, *Wrow;         // global [LW_ROWS][WAVE] (x, v): the LP rows L_k / W_k (lp_domains)
     int *off, *cnt, *wc, *lc;     // LDS [H + 1]: pool offset of V_k, its values m (m + 1 breakpoints),
                                   //   points of the W row / L row of x_k (lp_domains)
@@ -3496,7 +3495,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         // interval of the list's last point at or before it (running per-list counts, their chunk
         // offsets by one block scan), pruned by L_k -- and the compaction of the intervals of [dl, dh].
         int res = 1, tot = 0;
-        auto stage = [&](const auto* Bk, const auto* Vk, auto* I0, auto* I1, auto* VAL) {
+        auto stage = [&](const auto* Bk, const auto* Vk, auto* I0, auto* I1) {
             auto P = [&](int u, int i) { return (Bk[i] - g * (double)u - C) * iA; };
             auto uof = [](int id) { return id >> 24; };
             auto key = [&](int id) { return P(uof(id), id & 0xFFFFFF); };
@@ -3553,7 +3552,10 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
                 auto* ti = Is; Is = Id; Id = ti;
             }
             SPM(25);
-            // values: Is holds the merged points; VAL receives each one's interval value
+            // values: Is holds the merged points; the free buffer receives each one's interval value as a
+            // code j << 24 | idx (the value is q j + V_{k+1}[idx], recomputed bit-identically; -1: +inf)
+            auto* const VAL = Id;
+            auto dec = [&](int c) -> double { return c < 0 ? INFINITY : fma(q, (double)(c >> 24), Vk[c & 0xFFFFFF]); };
             const int per = (Mc + NT - 1) / NT;
             const int p0 = min(Mc, tid * per), p1 = min(Mc, p0 + per);
             int cnt[STEP_MAXU];
@@ -3566,21 +3568,25 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             }
             block_excl_scan_vec<NT>(cnt, NU, Sb.xr, tid);     // points of each list before the chunk
             double cur[STEP_MAXU];
+            int cc[STEP_MAXU];
 #pragma unroll
             for (int j = 0; j < STEP_MAXU; ++j) {
                 const int idx = Sb.rng[j] + cnt[j] - 1;   // (j < NU: rng is defined)
-                cur[j] = (j < NU && cnt[j] >= 1 && idx < m) ? fma(q, (double)j, Vk[idx]) : INFINITY;
+                const bool ok = j < NU && cnt[j] >= 1 && idx < m;
+                cur[j] = ok ? fma(q, (double)j, Vk[idx]) : INFINITY;
+                cc[j] = ok ? (j << 24) | idx : -1;
             }
             for (int p = p0; p < p1; ++p) {
                 const int id = Is[p], u = uof(id), i = id & 0xFFFFFF;
                 const double v = i < m ? fma(q, (double)u, Vk[i]) : INFINITY;
                 double best = INFINITY;
+                int bc = -1;
 #pragma unroll
                 for (int j = 0; j < STEP_MAXU; ++j) {
-                    if (j == u) cur[j] = v;
-                    best = fmin(best, cur[j]);
+                    if (j == u) { cur[j] = v; cc[j] = i < m ? id : -1; }
+                    if (cur[j] < best) { best = cur[j]; bc = cc[j]; }
                 }
-                VAL[p] = best;
+                VAL[p] = bc;
             }
             __syncthreads();
             SPM(26);
@@ -3591,7 +3597,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             const int pt = (T + NT - 1) / NT;
             const int t0 = min(T, tid * pt), t1 = min(T, t0 + pt);
             auto start = [&](int t) { return t == 0 ? dl : t >= T ? dh : key(Is[jl + t - 1]); };
-            auto raw = [&](int t) { return t == 0 ? (jl > 0 ? VAL[jl - 1] : INFINITY) : VAL[jl + t - 1]; };
+            auto raw = [&](int t) { return t == 0 ? (jl > 0 ? dec(VAL[jl - 1]) : INFINITY) : dec(VAL[jl + t - 1]); };
             // the pruning: min of the convex L_k over [a, b] is L at the clamp of its minimiser (+inf outside
             // its domain), by a table pointer that only moves right along the chunk
             const double xm = prune ? Sb.lt[3 * WAVE] : 0.0, lmin = prune ? Sb.lt[3 * WAVE + 1] : 0.0;
@@ -3657,24 +3663,22 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             walk([&](double s_, double v_) { OB[o] = s_; OV[o] = v_; ++o; });
         };
         // the pool: V_{k+1}'s breakpoints (and values when they fit too), then the merge buffers when
-        // they fit as well (ids i32 x 2, values f64)
+        // they fit as well (ids i32 x 2; the free one then holds the values' codes)
         const bool lds_v = staged && 16 * np + 32 <= Sb.spb;
-        const bool lds_m = staged && 8 * (lds_v ? 2 : 1) * np + 16 * Mc + 48 <= Sb.spb;
+        const bool lds_m = staged && 8 * (lds_v ? 2 : 1) * np + 8 * Mc + 32 <= Sb.spb;
         if (lds_v) {
             double* const vs = bs + np;
             for (int i = tid; i < m; i += NT) vs[i] = Vg[i];
         }
         SPM(24);
         if (lds_m) {
-            const int ob = (8 * (lds_v ? 2 : 1) * np + 15) & ~15, oi = (ob + 8 * Mc + 15) & ~15;
-            double* const vl = reinterpret_cast<double*>(Sb.sp + ob);
-            int* const i0 = reinterpret_cast<int*>(Sb.sp + oi);
-            if (lds_v) stage(bs, bs + np, i0, i0 + Mc, vl);
-            else stage(bs, Vg, i0, i0 + Mc, vl);
+            int* const i0 = reinterpret_cast<int*>(Sb.sp + ((8 * (lds_v ? 2 : 1) * np + 15) & ~15));
+            if (lds_v) stage(bs, bs + np, i0, i0 + Mc);
+            else stage(bs, Vg, i0, i0 + Mc);
         } else if (staged) {
-            stage(bs, Vg, Sb.GIA, Sb.GIB, Sb.GKA);
+            stage(bs, Vg, Sb.GIA, Sb.GIB);
         } else {
-            stage(Bg, Vg, Sb.GIA, Sb.GIB, Sb.GKA);
+            stage(Bg, Vg, Sb.GIA, Sb.GIB);
         }
         if (res != 1) return res;
         double* const OB = Sb.PB + top;
@@ -3683,7 +3687,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
 #ifdef DRAGG_STEP_PROF
         if (tid == 0 && !feas_only) {
             X[14 * 8 + S_PAD] += (double)np; X[15 * 8 + S_PAD] = fmax(X[15 * 8 + S_PAD], (double)np);
-            X[16 * 8 + S_PAD] += (8 * np > Sb.spb ? 1.0 : 0.0) + (8 * np + 16 * Mc + 48 > Sb.spb ? 1000.0 : 0.0);
+            X[16 * 8 + S_PAD] += (8 * np > Sb.spb ? 1.0 : 0.0) + (16 * np + 8 * Mc + 32 > Sb.spb ? 1000.0 : 0.0);
             X[18 * 8 + S_PAD] += (double)Mc;
         }
 #endif
@@ -3871,10 +3875,9 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 char* const sb = reinterpret_cast<char*>(smem);
                 double* const sw = reinterpret_cast<double*>(ws + narrow_region_offset(N, H) +
                                                              (size_t)(slot + (a.pred ? narrow_slots(N) : 0)) * step_slot_bytes());
-                int* const swi = reinterpret_cast<int*>(sw + 2 * (size_t)POOL_CAP + 2 * (size_t)MC_CAP);
+                int* const swi = reinterpret_cast<int*>(sw + 2 * (size_t)POOL_CAP);
                 double2* const swr = reinterpret_cast<double2*>(swi + 2 * (size_t)MC_CAP);
-                const StepBufs SB{sw, sw + POOL_CAP, sw + 2 * (size_t)POOL_CAP, sw + 2 * (size_t)POOL_CAP + MC_CAP,
-                                  swi, swi + MC_CAP, swr, swr + (size_t)LW_ROWS * WAVE,
+                const StepBufs SB{sw, sw + POOL_CAP, swi, swi + MC_CAP, swr, swr + (size_t)LW_ROWS * WAVE,
                                   reinterpret_cast<int*>(sb + nl.off), reinterpret_cast<int*>(sb + nl.cnt),
                                   reinterpret_cast<int*>(sb + nl.wc), reinterpret_cast<int*>(sb + nl.lc),
                                   reinterpret_cast<int*>(sb + nl.red), reinterpret_cast<int*>(sb + nl.xr),

@@ -166,7 +166,7 @@ def test_size_queries_without_gpu(lib_path):
     # then (256-aligned) the [N] i32 list (+ length) the mid launch hands to the big one and
     # (256-aligned) the mid launch's back-pointer rows [2048 blocks][H][NF_MID = 384] u16, then
     # (256-aligned) the predicted narrow homes' list [N] i32 (+ length, take counter) and flags [N] i32
-    slot = (2 * 2 ** 20 + 2 * 8 * 32768) * 8 + 2 * 8 * 32768 * 4 + 2 * 256 * 64 * 16
+    slot = 2 * 2 ** 20 * 8 + 2 * 8 * 32768 * 4 + 2 * 256 * 64 * 16
     ml_off = (nr_off + 2 * 16 * slot + 255) // 256 * 256
     mr_off = (ml_off + 101 * 4 + 255) // 256 * 256
     pl_off = (mr_off + 2048 * 24 * 384 * 2 + 255) // 256 * 256
