@@ -44,6 +44,7 @@ constexpr int NTB_HOT = 64;           // key / cost buckets per stage of the hot
 constexpr int NTB = 192;              // ... of the second launch's regular front DP and round_lp
 constexpr int NTB_BIG = 256;          // ... of the big exact pass (fronts up to NF_BIG)
 constexpr int NT_STEPS = 512;            // threads of a DM_NARROW block (8 waves)
+constexpr double STEP_U_FRAC = 0.75;     // the step-function DP's first bound: lb + this (ub - lb)
 constexpr int NARROW_SLOTS = 16;         // blocks of the persistent DM_NARROW launch
 // the exact step-function DP (dp_steps, DM_NARROW)
 constexpr int NP_CAP = 32768;             // breakpoints of one V_k
@@ -1606,7 +1607,7 @@ __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
     o.dhi = take(8 * (H + 1), 8);
     o.xv = take(8 * STEP_MAXU, 8);
     o.lt = take(8 * (3 * WAVE + 2), 16);
-    // the pool takes what is left of the CU's LDS (>= the waves' PL tables of lp_domains)
+    // the pool takes what is left of the CU's LDS (>= the waves' PL tables of lp_cut)
     o.sp = take(0, 16);
     o.spb = max(NT_STEPS / 64 * 6 * WAVE * 8, ((160 * 1024 - 256) - o.sp - 64) / 64 * 64);
     p = o.sp + o.spb;
@@ -3110,7 +3111,7 @@ DEV bool battery_lp(const Home& h, LdsD& L, int lane) {
 // Only the states that can lie on an optimal path are needed: with U >= the optimum (the cost of
 // a schedule the caller holds, or of the feasibility pass's schedule), the domain of V_k is cut to
 // D_k = {x : L_k(x) + W_k(x) <= U}, L_k the LP cost-to-reach of x_k from x_0 and W_k the LP
-// cost-to-go (duties continuous: both convex piecewise linear lower bounds, lp_domains), an
+// cost-to-go (duties continuous: both convex piecewise linear lower bounds, lp_rows / lp_cut), an
 // interval that holds every optimal state.  The cut DP's value is >= the true V_k everywhere and
 // equal along every optimal path, so the recovered schedule is the uncut DP's (the same lowest-duty
 // rule picks among the same optimal continuations); measured on the bench's narrow tanks: 3-15x
@@ -3193,9 +3194,9 @@ DEV int block_excl_max(int v, int* red, int tid) {      // max over the threads 
 struct StepBufs {
     double *PB, *PV;              // global [POOL_CAP]: breakpoints / values of V_k, stage after stage
     int *GIA, *GIB;               // global [MC_CAP]: a stage's point ids (u << 24 | i), ping-pong, past the LDS pool
-    double2 *Lrow, *Wrow;         // global [LW_ROWS][WAVE] (x, v): the LP rows L_k / W_k (lp_domains)
+    double2 *Lrow, *Wrow;         // global [LW_ROWS][WAVE] (x, v): the LP rows L_k / W_k (lp_rows / lp_cut)
     int *off, *cnt, *wc, *lc;     // LDS [H + 1]: pool offset of V_k, its values m (m + 1 breakpoints),
-                                  //   points of the W row / L row of x_k (lp_domains)
+                                  //   points of the W row / L row of x_k (lp_rows / lp_cut)
     int *red;                     // LDS [32] scan scratch (two scans of a stage: [0, 16), [16, 32))
     int *xr;                      // LDS [NT / 64][STEP_MAXU] vector-scan scratch
     int *rng;                     // LDS [4 STEP_MAXU + 8]: per-list index ranges of a stage, run offsets
@@ -3205,7 +3206,7 @@ struct StepBufs {
     double *lt;                   // LDS [3][WAVE] + 2: L_k as a table (points, values, slopes), its
                                   //   minimiser and minimum (the cost pruning)
     char* sp;                     // LDS pool [spb] bytes: per stage V_{k+1} (B, V) and the merge buffers
-    int spb;                      //   (lp_domains: the waves' PL tables)
+    int spb;                      //   (lp_cut: the waves' PL tables)
 };
 
 // exclusive prefix sums over the NT threads of the block of v[0..n) (n <= STEP_MAXU), in place
@@ -3257,8 +3258,8 @@ DEV double pl_tab(const double* T, int m, double x) {
 //   crosses U, widened past rounding).  A row that would pass 64 points, or an empty cut, leaves
 //   the stages it covers uncut (-inf, +inf).  Every thread of the block calls it.
 template <int NT>
-DEV void lp_domains(const StepBufs& Sb, const double* cA, const double* cC, const double* cq, int H, int S, double g,
-                    double x0, double lo0, double hi0, double lo, double hi, double U, int tid) {
+DEV void lp_rows(const StepBufs& Sb, const double* cA, const double* cC, const double* cq, int H, int S, double g,
+                 double x0, double lo0, double hi0, double lo, double hi, int tid) {
     static_assert(NT >= 2 * WAVE, "two waves build the rows");
     const int lane = tid & (WAVE - 1), wid = tid / WAVE;
     auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
@@ -3338,6 +3339,23 @@ DEV void lp_domains(const StepBufs& Sb, const double* cA, const double* cC, cons
         }
     }
     __syncthreads();
+}
+// the minimum of L_H: the chain's LP relaxation optimum (every thread; +inf without the row)
+DEV double lp_bound(const StepBufs& Sb, int H, int tid) {
+    const int lane = tid & (WAVE - 1), ml = Sb.lc[H];
+    const double v = lane < ml ? Sb.Lrow[H * WAVE + lane].y : INFINITY;
+    return dpp_reduce(v, [](double a, double b) { return fmin(a, b); });
+}
+// the cut domains D_k = {L_k + W_k <= U} from the rows of lp_rows (any U, again and again)
+template <int NT>
+DEV void lp_cut(const StepBufs& Sb, int H, double U, int tid) {
+    const int lane = tid & (WAVE - 1), wid = tid / WAVE;
+    auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
+    const double2* const Lrow = Sb.Lrow;
+    const double2* const Wrow = Sb.Wrow;
+    const int* const lcnt = Sb.lc;
+    for (int k = tid; k <= H; k += NT) { Sb.dlo[k] = -INFINITY; Sb.dhi[k] = INFINITY; }
+    __syncthreads();
     // the sublevel set of every stage, one wave per stage (its own two PL tables in bs)
     double* const TL = reinterpret_cast<double*>(Sb.sp) + wid * 6 * WAVE;
     double* const TW = TL + 3 * WAVE;
@@ -3381,8 +3399,8 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
     // +inf elsewhere; equal neighbours merge, so V_k is the feasible set as a union of a few intervals.
     // Its breakpoints are the finite region's ends of the full DP's (the same preimage arithmetic),
     // so the feasibility verdict is the full DP's -- at a fraction of its cost (no cost steps).
-    // cut_domains: V_k only on Sb.dlo/dhi (lp_domains); else those are ignored.  U < inf (with
-    // cut_domains): V_k is also set to +inf on every interval where L_k (lp_domains' cost-to-reach rows)
+    // cut_domains: V_k only on Sb.dlo/dhi (lp_rows / lp_cut); else those are ignored.  U < inf (with
+    // cut_domains): V_k is also set to +inf on every interval where L_k (lp_rows' cost-to-reach rows)
     // plus V_k exceeds U -- no state there lies on a schedule of cost <= U.
     auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
     auto boxlo = [&](int k) { const double b = k == 0 ? lo0 : lo; return b - tw(b); };   // box of x_{k+1}
@@ -3942,19 +3960,45 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                     for (int k = lane & (WAVE - 1); k < H; k += WAVE) qabs += fabs(D.cq[k]) * h.S;
                     qabs = dpp_sum(qabs);
                     __syncthreads();
-                    const double U = ub + TOL_P * (1.0 + fabs(ub) + qabs);
-                    lp_domains<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, U, lane);
-#ifdef DRAGG_STEP_PROF
-                    if (lane == 0) {
-                        int ncut = 0;
-                        for (int k = 1; k <= H; ++k) ncut += (SB.dlo[k] > -INFINITY) ? 1 : 0;
-                        D.x[17 * 8 + S_PAD] += 100.0 * ncut;
-                        D.x[20 * 8 + S_PAD] = ub;
+                    auto Umargin = [&](double u_) { return u_ + TOL_P * (1.0 + fabs(u_) + qabs); };
+                    const double U = Umargin(ub);
+                    lp_rows<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, lane);
+                    // A first try at a smaller bound: U1 = lb + STEP_U_FRAC (ub - lb), lb the LP relaxation.  The
+                    // cut DP is exact whenever its bound is >= the optimum, and a schedule it returns costs >= the
+                    // optimum, so one costing <= U1 IS the optimum; otherwise (U1 below the optimum: no schedule, or
+                    // a dearer one) the DP runs again at U.  The work grows fast with the bound (the bench's narrow
+                    // tanks: 2.4x the merge points at the bucketed schedule's cost, ~15 % above the optimum, than
+                    // at the optimum), and the optimum lies 0.55-0.7 of the way from lb to that cost there.
+                    const double lb = lp_bound(SB, H, lane);
+                    bool first = false;
+                    if (lb < ub) {
+                        const double U1 = Umargin(lb + STEP_U_FRAC * (ub - lb));
+                        if (U1 < U) {
+                            lp_cut<NT>(SB, H, U1, lane);
+                            PMARK(11);
+                            first = steps(false, true, U1) == 1 && sched_cost() <= U1;
+                            PMARK(12);
+                            __syncthreads();
+                        }
                     }
+#ifdef DRAGG_STEP_PROF
+                    if (lane == 0) { D.x[20 * 8 + S_PAD] = ub; if (first) D.x[17 * 8 + S_PAD] += 1e6; }
 #endif
-                    PMARK(11);
-                    r = steps(false, true, U);              // V_k on the cut domains, pruned by L_k + V_k <= U
-                    PMARK(12);
+                    if (first) {
+                        r = 1;
+                    } else {
+                        lp_cut<NT>(SB, H, U, lane);
+#ifdef DRAGG_STEP_PROF
+                        if (lane == 0) {
+                            int ncut = 0;
+                            for (int k = 1; k <= H; ++k) ncut += (SB.dlo[k] > -INFINITY) ? 1 : 0;
+                            D.x[17 * 8 + S_PAD] += 100.0 * ncut;
+                        }
+#endif
+                        PMARK(11);
+                        r = steps(false, true, U);              // V_k on the cut domains, pruned by L_k + V_k <= U
+                        PMARK(12);
+                    }
                     if (r == -6) {                          // (rounding put the optimum outside a cut: uncut)
 #ifdef DRAGG_STEP_PROF
                         if (lane == 0) D.x[17 * 8 + S_PAD] += 1.0;
