@@ -44,7 +44,7 @@ constexpr int NTB_HOT = 64;           // key / cost buckets per stage of the hot
 constexpr int NTB = 192;              // ... of the second launch's regular front DP and round_lp
 constexpr int NTB_BIG = 256;          // ... of the big exact pass (fronts up to NF_BIG)
 constexpr int NT_STEPS = 512;            // threads of a DM_NARROW block (8 waves)
-constexpr double STEP_U_FRAC = 0.75;     // the step-function DP's first bound: lb + this (ub - lb)
+constexpr double STEP_U_FRAC = 0.65;     // the step-function DP's first bound: lb + this (ub - lb)
 constexpr int NARROW_SLOTS = 16;         // blocks of the persistent DM_NARROW launch
 // the exact step-function DP (dp_steps, DM_NARROW)
 constexpr int NP_CAP = 32768;             // breakpoints of one V_k
