@@ -1203,8 +1203,6 @@ struct KArgs {
     const double* noise;
     int t;
     int force_steps;       // diagnostic (DRAGG_FORCE_STEP_DP=1): every home to the exact step DP
-    int pred;              // DM_NARROW: 1 = the launch of the predicted narrow homes (side stream)
-    const int* pflag;      // DM_FRONT: [N] 1 = a predicted narrow home, solved by the side launch (or NULL)
 };
 
 // --------------------------------------------------------------------------------------
@@ -1477,21 +1475,13 @@ __host__ __device__ inline size_t narrow_region_offset(int N, int H) {
 // then the list of homes the mid launch hands to the big one ([N] i32 + length) and (256-aligned)
 // the mid launch's back-pointer rows [MID_SLOTS_MAX][H][NF_MID] u16
 __host__ __device__ inline size_t mid_list_offset(int N, int H) {
-    return (narrow_region_offset(N, H) + (size_t)2 * narrow_slots(N) * step_slot_bytes() + 255) / 256 * 256;
+    return (narrow_region_offset(N, H) + (size_t)narrow_slots(N) * step_slot_bytes() + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t mid_region_offset(int N, int H) {
     return (mid_list_offset(N, H) + (size_t)(N + 2) * sizeof(int) + 255) / 256 * 256;
 }
-// then (256-aligned) the list of the homes predicted narrow ([N] i32 + length + take counter) and
-// their flags [N] i32 (predict_kernel -> the side DM_NARROW launch; the hot launch skips them)
-__host__ __device__ inline size_t pred_list_offset(int N, int H) {
-    return (mid_region_offset(N, H) + (size_t)MID_SLOTS_MAX * H * NF_MID * sizeof(uint16_t) + 255) / 256 * 256;
-}
-__host__ __device__ inline size_t pred_flag_offset(int N, int H) {
-    return (pred_list_offset(N, H) + (size_t)(N + 2) * sizeof(int) + 255) / 256 * 256;
-}
 __host__ __device__ inline size_t direct_workspace_bytes(int N, int H) {
-    return pred_flag_offset(N, H) + (size_t)N * sizeof(int);
+    return mid_region_offset(N, H) + (size_t)MID_SLOTS_MAX * H * NF_MID * sizeof(uint16_t);
 }
 
 struct DirectLayout {
@@ -3892,7 +3882,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 const NarrowLayout nl = narrow_layout(H, a.d.sub_steps);
                 char* const sb = reinterpret_cast<char*>(smem);
                 double* const sw = reinterpret_cast<double*>(ws + narrow_region_offset(N, H) +
-                                                             (size_t)(slot + (a.pred ? narrow_slots(N) : 0)) * step_slot_bytes());
+                                                             (size_t)slot * step_slot_bytes());
                 int* const swi = reinterpret_cast<int*>(sw + 2 * (size_t)POOL_CAP);
                 double2* const swr = reinterpret_cast<double2*>(swi + 2 * (size_t)MC_CAP);
                 const StepBufs SB{sw, sw + POOL_CAP, swi, swi + MC_CAP, swr, swr + (size_t)LW_ROWS * WAVE,
@@ -3912,34 +3902,10 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                     for (int k = lane & (WAVE - 1); k < H; k += WAVE) c += D.cq[k] * D.x[k * 8 + sv];
                     return dpp_sum(c);
                 };
-                // a predicted home (side launch) starts from chain 0, the indoor air, which is narrow in
-                // practice only where the prediction flags the wrong chain: the regular exact front DP (all
-                // waves of the block; its W table and exchange area in the pool) solves it far faster than the
-                // step-function DP (which takes it where the front DP does not apply)
-                if (a.pred && h.S == 6 && chain == 0) {
-                    double* const wl = reinterpret_cast<double*>(SB.sp);
-                    char* const xch = SB.sp + 3 * WAVE * sizeof(double);
-                    double2* const wg = reinterpret_cast<double2*>(ws + w_region_offset(N, H)) + (size_t)home * (H + 1) * WAVE;
-                    const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
-                                       wg, wl, wl + WAVE, wl + 2 * WAVE, xch};
-                    const int rf = dp_front<6, NF, NF_BOUND, NB_CAP, NTB, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv,
-                                                                        rl_prices, INFINITY, nullptr);
-                    __syncthreads();
-                    if (rf >= 0) {
-                        ok = rf == 1;
-                        if (!ok) int_path |= 1 << (13 + chain);
-                        continue;
-                    }
-                }
                 // an upper bound on the chain's optimum: the bucketed schedule the mid / big launch left in the
                 // solution rows; without one the feasibility pass (all duty costs 0: the feasible set as a few
                 // intervals, microseconds) decides whether any schedule exists and gives one
                 double ub = (chain == first_chain && (eflags & BK_OK)) ? sched_cost() : INFINITY;
-                // a predicted home has no bucketed schedule yet: the bucketed DP gives one (a bound within a
-                // few % of the optimum: far smaller cut domains than the feasibility pass's schedule)
-                if (a.pred && h.S == 6 && !(ub < INFINITY) &&
-                    dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv))
-                    ub = sched_cost();
 #ifdef DRAGG_STEP_PROF
                 unsigned long long pt = __builtin_amdgcn_s_memtime();
                 auto pmark = [&](int slot_) {
@@ -4154,8 +4120,7 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
     char* const ws = reinterpret_cast<char*>(a.p.workspace);
     const int N = a.d.n_homes, H = a.d.horizon;
     if (MODE == DM_FRONT) {
-        // (a home predicted narrow is the side launch's: nothing of it is read or written here)
-        if ((int)blockIdx.x < N && !(a.pflag && a.pflag[blockIdx.x])) solve_direct<EXPLICIT, MODE, NW>(a, blockIdx.x, smem, 0, 0);
+        if ((int)blockIdx.x < N) solve_direct<EXPLICIT, MODE, NW>(a, blockIdx.x, smem, 0, 0);
         return;
     }
     // persistent: block b solves listed home b first, then takes the next ones off a shared counter
@@ -4163,7 +4128,7 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
     // ms per action against a static stride), each with its own scratch rows in the workspace (slot
     // b); blocks past the list's length leave at once, every block reaches its end and exits
     const size_t lo = MODE == DM_MID ? defer_offset(N, H) : MODE == DM_BUCKET ? mid_list_offset(N, H)
-                    : a.pred ? pred_list_offset(N, H) : narrow_list_offset(N, H);
+                    : narrow_list_offset(N, H);
     int* const list = reinterpret_cast<int*>(ws + lo);
     const int cnt = min(list[N], N);
     __shared__ int take;
@@ -4179,110 +4144,11 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
 }
 
 // the three device lists' (length, take counter) pairs to zero before a step's launches
-__global__ void reset_lists_kernel(int* a, int* b, int* c, int* d) {
+__global__ void reset_lists_kernel(int* a, int* b, int* c) {
     const int i = threadIdx.x;
     if (i < 2) a[i] = 0;
     else if (i < 4) b[i - 2] = 0;
     else if (i < 6) c[i - 4] = 0;
-    else if (i < 8 && d) d[i - 6] = 0;
-}
-
-// Which homes' chains may have a feasible set narrower than one duty step (the front DP's dominance
-// does not hold there; the exact step-function DP solves them): one thread per home, before the hot
-// launch, so that those homes are solved by a DM_NARROW launch on a side stream CONCURRENTLY with the
-// hot launch instead of after it.  The front DP's narrowness test (dp_front (b)) looks at the backward
-// hulls F_H .. F_2, which depend on the stage maps and the boxes only -- not on the initial state.  The
-// tank chain's C_k holds e T_{k+1} (the indoor-air optimum, not known yet): T_{k+1} is taken anywhere in
-// its box, the hull ends carried as intervals, and a home is flagged when the narrowest possible hull
-// is narrower than a duty step (conservative: a flagged home that is not narrow is solved exactly all
-// the same).  The indoor-air chain is tested too, with the larger of the two modes' duty steps.
-template <bool EXPLICIT>
-__global__ void predict_kernel(KArgs a, int* plist, int* pflag) {
-    const int home = blockIdx.x * blockDim.x + threadIdx.x;
-    const int N = a.d.n_homes;
-    if (home >= N) return;
-    const int H = a.d.horizon, dt = a.d.dt, S = a.d.sub_steps;
-    Home h;
-    h.H = H; h.S = S; h.dt = dt; h.winter = true;
-    load_params(h, a.p.params, N, home);
-    derive(h);
-    auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
-    // the step's draw sizes (as the prologue: mpc_calc.py:193-204) and outdoor temperatures
-    const int lag = H / dt + 1, nraw = lag * dt, base_hour = (EXPLICIT ? 0 : a.t) / dt;
-    auto rawv = [&](int idx) -> double {
-        const int hh = base_hour + idx / dt - lag;
-        const double v = (hh >= 0 && hh < a.d.n_draw_hours) ? a.p.draw_hourly[(size_t)hh * N + home] : 0.0;
-        return v / dt;
-    };
-    auto draw = [&](int i) -> double {
-        if (EXPLICIT) return a.ex.draw[(size_t)i * N + home];
-        if (i < dt) return rawv(i);
-        if (i + 1 < nraw) return ((rawv(i - 1) + rawv(i)) + rawv(i + 1)) / 3.0;
-        return (rawv(i - 1) + rawv(i)) / 2.0;
-    };
-    auto oat = [&](int i) -> double {
-        return EXPLICIT ? a.ex.oat[(size_t)i * N + home] : a.p.oat[a.p.start_index + a.t + i];
-    };
-    bool narrow = false;
-    if (H >= 2) {
-        // tank chain: x_{k+1} = A_k x_k + e T_{k+1} + c_k + f u,  T_{k+1} in [Tmin, Tmax]
-        const double g = h.f, gmin = fmin(0.0, g * S), gmax = fmax(0.0, g * S);
-        const double eTlo = h.e * (h.Tmin - tw(h.Tmin)), eThi = h.e * (h.Tmax + tw(h.Tmax));
-        const double bl = h.Twmin - tw(h.Twmin), bh = h.Twmax + tw(h.Twmax);
-        double llo = bl, lhi = bl, ulo = bh, uhi = bh;
-        for (int k = H - 1; k >= 1 && !narrow; --k) {
-            if (ulo - lhi < fabs(g)) { narrow = true; break; }
-            if (k == 1) break;                         // (F_1 is not tested: its box is the state's)
-            const double df = draw(k + 1) / h.V, rem = 1 - df, d15 = df * TAP;
-            const double A = rem + (-rem * h.iRw) * 3600 * h.inv_w;
-            const double c = d15 + ((-d15) * h.iRw) * 3600 * h.inv_w;
-            if (!(A > 0.0)) break;
-            const double iA = 1.0 / A, Clo = eTlo + c, Chi = eThi + c;
-            double nllo = fmax((llo - Chi - gmax) * iA, bl), nlhi = fmax((lhi - Clo - gmax) * iA, bl);
-            double nulo = fmin((ulo - Chi - gmin) * iA, bh), nuhi = fmin((uhi - Clo - gmin) * iA, bh);
-            nllo -= 2 * tw(nllo); nlhi -= 0.5 * tw(nlhi); nulo += 0.5 * tw(nulo); nuhi += 2 * tw(nuhi);
-            llo = nllo; lhi = nlhi; ulo = nulo; uhi = nuhi;
-            if (llo > uhi) break;                      // (no schedule: decided on the regular path)
-        }
-        // indoor air: C_k = oat_{k+1} / R 3600 inv_c, in the season's mode (the prologue's draw,
-        // mpc_calc.py:220-223, 303-309; a wrong-season mode is often nearly infeasible, i.e. narrow)
-        bool winter;
-        if (EXPLICIT) {
-            winter = a.ex.winter[home] != 0;
-        } else {
-#pragma clang fp contract(off)
-            const int s0 = a.p.start_index + a.t;
-            double mx = a.p.oat[s0];
-            for (int k = 0; k < H; ++k) {
-                double z;
-                if (a.noise) z = a.noise[(size_t)k * N + home];
-                else {
-                    double z0, z1;
-                    normal_pair(a.p.seed, a.p.home_offset + home * max(a.p.home_stride, 1), a.t, k >> 1, &z0, &z1);
-                    z = (k & 1) ? z1 : z0;
-                }
-                mx = fmax(mx, a.p.oat[s0 + k + 1] + pow(1.1, (double)k) * z);
-            }
-            winter = mx <= 30.0;
-        }
-        const double tl = h.Tmin - tw(h.Tmin), th = h.Tmax + tw(h.Tmax);
-        for (int mode = winter ? 0 : 1; mode == (winter ? 0 : 1) && !narrow; ++mode) {
-            const double gT = mode == 0 ? h.Ph * 3600 * h.inv_c : -(h.Pc * 3600 * h.inv_c);
-            const double gmn = fmin(0.0, gT * S), gmx = fmax(0.0, gT * S);
-            double l = tl, u = th;
-            for (int k = H - 1; k >= 1; --k) {
-                if (u - l < fabs(gT)) { narrow = true; break; }
-                if (k == 1) break;
-                const double C = oat(k + 1) * h.iR * 3600 * h.inv_c, iA = 1.0 / h.aT;
-                l = fmax((l - C - gmx) * iA, tl);
-                u = fmin((u - C - gmn) * iA, th);
-                l -= 2 * tw(l); u += 2 * tw(u);
-                if (l > u) break;
-            }
-        }
-    }
-    pflag[home] = narrow ? 1 : 0;
-    if (narrow) plist[atomicAdd(plist + N, 1)] = home;
 }
 
 // collect_data's three sums (aggregator.py:728-755) in one 1024-thread block: 16 waves of
@@ -4373,14 +4239,13 @@ constexpr int MAX_DEV = 64;
 
 // Diagnostic knobs, read once per process (not on every step): DRAGG_WAVES_PER_HOME=1|2|4 forces
 // the hot launch's waves per home (A/B runs); DRAGG_FORCE_STEP_DP=1 sends every home's chains to
-// the step-function DP (DM_NARROW); DRAGG_PREDICT=1 turns the narrow-home prediction (and its side
-// stream) on -- measured slower at 10k homes and at the 8-way shard (the side launch's step DP outlasts
-// the hot launch; the prediction costs ~0.1 ms at 1,250 homes), so off by default.  Unset: one wave per
-// home, the regular launch order.
+// the step-function DP (DM_NARROW).  Unset: one wave per home, the regular launch order.  (Round 4
+// measured and removed a prediction of the narrow homes before the hot launch with their step-function DP
+// on a high-priority side stream beside it: 2.81 against 2.29 ms over the full day -- the side solves
+// outlast the hot launch and take CUs from it -- and ~0.1 ms of prediction per step at 1,250 homes.)
 struct Knobs {
     int waves = 1;
     int force_steps = 0;
-    int no_predict = 1;
 };
 const Knobs& knobs() {
     static const Knobs k = [] {
@@ -4389,8 +4254,6 @@ const Knobs& knobs() {
         if (w && (w[0] == '1' || w[0] == '2' || w[0] == '4') && w[1] == 0) r.waves = w[0] - '0';
         const char* f = getenv("DRAGG_FORCE_STEP_DP");
         r.force_steps = (f && f[0] == '1') ? 1 : 0;
-        const char* pr_ = getenv("DRAGG_PREDICT");
-        r.no_predict = (pr_ && pr_[0] == '1') ? 0 : 1;
         return r;
     }();
     return k;
@@ -4425,28 +4288,6 @@ int mid_slots(int dev, int H, int S) {
     return slots;
 }
 
-// The side stream of the predicted narrow homes (one per device, the device's highest priority, so
-// that its workgroups take their CUs before the hot launch fills them) and the two events that order
-// it after the prediction and the caller's stream after it.  Created on first use.
-struct Side {
-    hipStream_t st = nullptr;
-    hipEvent_t pred_done = nullptr, side_done = nullptr;
-    bool ok = false, tried = false;
-};
-Side& side_stream(int dev) {
-    static Side sd[MAX_DEV];
-    Side& x = sd[dev];
-    if (!x.tried) {
-        x.tried = true;
-        int lo = 0, hi = 0;
-        x.ok = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
-               hipStreamCreateWithPriority(&x.st, hipStreamNonBlocking, hi) == hipSuccess &&
-               hipEventCreateWithFlags(&x.pred_done, hipEventDisableTiming) == hipSuccess &&
-               hipEventCreateWithFlags(&x.side_done, hipEventDisableTiming) == hipSuccess;
-    }
-    return x;
-}
-
 template <bool EXPLICIT>
 int launch(const KArgs& a, hipStream_t s) {
     static int attr_dev[MAX_DEV][8] = {};
@@ -4461,34 +4302,12 @@ int launch(const KArgs& a, hipStream_t s) {
     int* const len = reinterpret_cast<int*>(wsb + defer_offset(N, a.d.horizon)) + N;
     int* const nlen = reinterpret_cast<int*>(wsb + narrow_list_offset(N, a.d.horizon)) + N;
     int* const blen = reinterpret_cast<int*>(wsb + mid_list_offset(N, a.d.horizon)) + N;
-    int* const plist = reinterpret_cast<int*>(wsb + pred_list_offset(N, a.d.horizon));
-    int* const pflag = reinterpret_cast<int*>(wsb + pred_flag_offset(N, a.d.horizon));
     KArgs b = a;
     b.force_steps = knobs().force_steps;
-    // narrow homes predicted ahead (int_mode round, S = 6: where the front DP runs at all)
-    Side& sd = side_stream(dev);
-    const bool predict = sd.ok && a.d.int_mode == DRAGG_INT_ROUND && a.d.sub_steps == 6 && !b.force_steps &&
-                         !knobs().no_predict;
     // each list's length and the persistent launch's take counter after it, in one tiny launch
     // (three 8-byte memsets cost three fills: ~13 us of a 0.49 ms step at 1,250 homes)
-    hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, nlen, blen, predict ? plist + N : nullptr);
+    hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, nlen, blen);
     if (hipGetLastError() != hipSuccess) return DRAGG_E_HIP;
-    if (predict) {
-        hipLaunchKernelGGL(predict_kernel<EXPLICIT>, dim3((N + 255) / 256), dim3(256), 0, s, b, plist, pflag);
-        if (hipGetLastError() != hipSuccess) return DRAGG_E_HIP;
-        // the side stream: after the prediction, the step-function DP of the predicted homes (their
-        // own workspace slots), concurrently with the hot / mid / big launches on the caller's stream
-        if (hipEventRecord(sd.pred_done, s) != hipSuccess || hipStreamWaitEvent(sd.st, sd.pred_done, 0) != hipSuccess)
-            return DRAGG_E_HIP;
-        KArgs c = b;
-        c.pred = 1;
-        const int rcs = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_NARROW, NT_STEPS / WAVE>, attr[5], c,
-                                      min(N, NARROW_SLOTS), NT_STEPS, (size_t)narrow_layout(a.d.horizon, a.d.sub_steps).bytes,
-                                      sd.st);
-        if (rcs) return rcs;
-        if (hipEventRecord(sd.side_done, sd.st) != hipSuccess) return DRAGG_E_HIP;
-        b.pflag = pflag;
-    }
     const size_t lds = kernel_lds_bytes(&a.d);
     const int nw = hot_waves();
 
@@ -4507,10 +4326,7 @@ int launch(const KArgs& a, hipStream_t s) {
     if (rc2) return rc2;
     const int rcn = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_NARROW, NT_STEPS / WAVE>, attr[5], b, min(N, NARROW_SLOTS),
                                   NT_STEPS, (size_t)narrow_layout(a.d.horizon, a.d.sub_steps).bytes, s);
-    if (rcn) return rcn;
-    // the step is complete on the caller's stream only with the side stream's work
-    if (predict && hipStreamWaitEvent(s, sd.side_done, 0) != hipSuccess) return DRAGG_E_HIP;
-    return DRAGG_OK;
+    return rcn;
 }
 
 }  // namespace

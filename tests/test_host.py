@@ -156,22 +156,19 @@ def test_size_queries_without_gpu(lib_path):
     # the second launch, then (256-aligned) the front DP's LP cost-to-go rows [N][H + 1][64] (x, v),
     # then (256-aligned) the second launch's back-pointer rows [512 blocks][H][NF_BIG = 2048] u16,
     # then (256-aligned) the [N] i32 list (+ length) of homes for the step-function DP launch and
-    # (256-aligned) its storage: 2 x min(N, 16) slots (the regular launch's and the side launch's of the
-    # predicted narrow homes) of ([2][2^20] + [2][8 x 32768] f64 + [2][8 x 32768] i32 + [2][256][64] (x, v))
+    # (256-aligned) its storage: min(N, 16) block slots of ([2][2^20] f64 breakpoints / values,
+    # [2][8 x 32768] i32 merge ids, [2][256][64] (x, v) LP rows)
     par = (100 * 24 * 336 * 2 + 255) // 256 * 256
     w_off = (par + 100 * 8 * 24 * 8 + 101 * 4 + 255) // 256 * 256
     big_off = (w_off + 100 * 25 * 64 * 16 + 255) // 256 * 256
     nl_off = (big_off + 512 * 24 * 2048 * 2 + 255) // 256 * 256
     nr_off = (nl_off + 101 * 4 + 255) // 256 * 256
     # then (256-aligned) the [N] i32 list (+ length) the mid launch hands to the big one and
-    # (256-aligned) the mid launch's back-pointer rows [2048 blocks][H][NF_MID = 384] u16, then
-    # (256-aligned) the predicted narrow homes' list [N] i32 (+ length, take counter) and flags [N] i32
+    # (256-aligned) the mid launch's back-pointer rows [2048 blocks][H][NF_MID = 384] u16
     slot = 2 * 2 ** 20 * 8 + 2 * 8 * 32768 * 4 + 2 * 256 * 64 * 16
-    ml_off = (nr_off + 2 * 16 * slot + 255) // 256 * 256
+    ml_off = (nr_off + 16 * slot + 255) // 256 * 256
     mr_off = (ml_off + 101 * 4 + 255) // 256 * 256
-    pl_off = (mr_off + 2048 * 24 * 384 * 2 + 255) // 256 * 256
-    pf_off = (pl_off + 102 * 4 + 255) // 256 * 256
-    assert ws == pf_off + 100 * 4
+    assert ws == mr_off + 2048 * 24 * 384 * 2
     lds_direct = lib.dragg_mpc_lds_bytes(ctypes.byref(d))
     assert 0 < lds_direct <= 13 * 1024                 # the hot launch: >= 12 homes per CU at H = 24
     d.horizon = 48

@@ -17,11 +17,9 @@ tail -1 $OUT/pytest.log
 grep -E "step-function|narrow-set" $OUT/pytest.log | head -4
 timeout -k 10 300 python3 bench.py --steps 96 --warmup 4 --cpu-seconds 0 > $OUT/full96.json 2> $OUT/full96.err || { echo BENCH_FAIL; tail -5 $OUT/full96.err; exit 1; }
 python3 -c "import json; d=json.load(open('$OUT/full96.json')); print('full96', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],4), 'ms/step')"
-for v in ${EXTRA:-nopred shard8}; do
+for v in ${EXTRA:-shard8}; do
   case $v in
-    pred) DRAGG_PREDICT=1 timeout -k 10 300 python3 bench.py --steps 96 --warmup 4 --cpu-seconds 0 > $OUT/$v.json 2> $OUT/$v.err || { echo BENCH_FAIL $v; tail -5 $OUT/$v.err; exit 1; } ;;
     shard8) timeout -k 10 300 python3 bench.py --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 > $OUT/$v.json 2> $OUT/$v.err || { echo BENCH_FAIL $v; tail -5 $OUT/$v.err; exit 1; } ;;
-    shard8p) DRAGG_PREDICT=1 timeout -k 10 300 python3 bench.py --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 > $OUT/$v.json 2> $OUT/$v.err || { echo BENCH_FAIL $v; tail -5 $OUT/$v.err; exit 1; } ;;
   esac
   python3 -c "import json; d=json.load(open('$OUT/$v.json')); print('$v', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],4), 'ms/step')"
 done
