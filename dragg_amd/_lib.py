@@ -91,7 +91,7 @@ class KernelInfo(ctypes.Structure):
 
 EXPORTS = ["dragg_mpc_abi_version", "dragg_mpc_strerror", "dragg_mpc_lds_bytes", "dragg_mpc_workspace_bytes",
            "dragg_mpc_kernel_info_get", "dragg_mpc_step",
-           "dragg_mpc_solve_explicit", "dragg_mpc_aggregate", "dragg_mpc_season_noise"]
+           "dragg_mpc_solve_explicit", "dragg_mpc_aggregate", "dragg_mpc_season_noise", "dragg_mpc_reload_knobs"]
 
 _LIB = None
 
@@ -121,6 +121,8 @@ def load(path=LIB_PATH):
                                              ctypes.POINTER(Explicit), ctypes.POINTER(Hash),
                                              ctypes.POINTER(Out), c_dp]
     lib.dragg_mpc_kernel_info_get.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(KernelInfo)]
+    lib.dragg_mpc_reload_knobs.argtypes = []
+    lib.dragg_mpc_reload_knobs.restype = None
     lib.dragg_mpc_aggregate.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Hash), c_dp, c_dp]
     lib.dragg_mpc_season_noise.argtypes = [ctypes.POINTER(Dims), ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
                                            ctypes.c_int32, c_dp, c_dp]
@@ -128,6 +130,12 @@ def load(path=LIB_PATH):
         raise DraggError("ABI version mismatch between dragg_amd and libdragg_mi355x.so")
     _LIB = lib
     return lib
+
+
+def reload_knobs():
+    """Re-read the diagnostic environment knobs (DRAGG_WAVES_PER_HOME, DRAGG_FORCE_STEP_DP): the library
+    reads them once when it loads, never per step."""
+    load().dragg_mpc_reload_knobs()
 
 
 def kernel_info(dims):

@@ -4247,17 +4247,16 @@ struct Knobs {
     int waves = 1;
     int force_steps = 0;
 };
-const Knobs& knobs() {
-    static const Knobs k = [] {
-        Knobs r;
-        const char* w = getenv("DRAGG_WAVES_PER_HOME");
-        if (w && (w[0] == '1' || w[0] == '2' || w[0] == '4') && w[1] == 0) r.waves = w[0] - '0';
-        const char* f = getenv("DRAGG_FORCE_STEP_DP");
-        r.force_steps = (f && f[0] == '1') ? 1 : 0;
-        return r;
-    }();
-    return k;
+Knobs read_knobs() {
+    Knobs r;
+    const char* w = getenv("DRAGG_WAVES_PER_HOME");
+    if (w && (w[0] == '1' || w[0] == '2' || w[0] == '4') && w[1] == 0) r.waves = w[0] - '0';
+    const char* f = getenv("DRAGG_FORCE_STEP_DP");
+    r.force_steps = (f && f[0] == '1') ? 1 : 0;
+    return r;
 }
+Knobs g_knobs = read_knobs();          // at library load; again only on dragg_mpc_reload_knobs()
+const Knobs& knobs() { return g_knobs; }
 
 // Waves per home of the hot launch: one (measured at 1,250 homes, the 8-GPU shard of the bench:
 // 0.495 / 0.53 / 0.80 ms per step at 1 / 2 / 4 waves per home -- a stage's fixed latency (ranges,
@@ -4393,6 +4392,8 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
     a.d = *dims; a.p = *prob; a.ex = *in; a.vals = hash->vals; a.fc = hash->fc; a.out = *out;
     return launch<true>(a, (hipStream_t)stream);
 }
+
+void dragg_mpc_reload_knobs(void) { g_knobs = read_knobs(); }
 
 int dragg_mpc_kernel_info_get(const dragg_mpc_dims* dims, dragg_mpc_kernel_info* info) {
     const int rc = check_dims(dims);

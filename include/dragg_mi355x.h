@@ -254,6 +254,11 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
                              const dragg_mpc_explicit* in, dragg_mpc_hash* hash,
                              dragg_mpc_out* out, void* stream);
 
+/* Diagnostic knobs, read from the environment when the library loads and again only here (never
+   per step): DRAGG_WAVES_PER_HOME=1|2|4 (the hot launch's waves per home; results bit-identical) and
+   DRAGG_FORCE_STEP_DP=1 (every chain through the step-function DP; tests).  Unset: the defaults. */
+void dragg_mpc_reload_knobs(void);
+
 /* Fill `info` for these dims (needs a GPU: queries the current device). */
 int dragg_mpc_kernel_info_get(const dragg_mpc_dims* dims, dragg_mpc_kernel_info* info);
 

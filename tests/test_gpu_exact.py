@@ -43,7 +43,8 @@ def _solve(d, mode="round"):
     b.vals.copy_(torch.tensor(vals))
     b.solve_explicit(**ex)
     torch.cuda.synchronize()
-    return dict(status=b.status.cpu().numpy(), fc=b.fc.cpu().numpy(), path=b.int_path.cpu().numpy() & L.PATH_APPROX_MASK, S=b.S)
+    ip = b.int_path.cpu().numpy()
+    return dict(status=b.status.cpu().numpy(), fc=b.fc.cpu().numpy(), path=ip & L.PATH_APPROX_MASK, raw_path=ip, S=b.S)
 
 
 def _thermal_cost(r, fc, i, S):
@@ -170,10 +171,12 @@ def test_step_function_dp_is_exact_on_every_record(name, gpu):
     d = F.load(name)
     ex = _exact()[name]
     os.environ["DRAGG_FORCE_STEP_DP"] = "1"
+    L.reload_knobs()                     # (the library reads its knobs at load, never per step)
     try:
         res = _solve(d, "round")
     finally:
         os.environ.pop("DRAGG_FORCE_STEP_DP", None)
+        L.reload_knobs()
     homes = {h["name"]: h for h in d["homes"]}
     n = 0
     for i, r in enumerate(d["records"]):
@@ -186,6 +189,7 @@ def test_step_function_dp_is_exact_on_every_record(name, gpu):
         assert res["path"][i] == 0, (name, i, res["path"][i])          # no approximation
         if not has:
             continue
+        assert res["raw_path"][i] & L.PATH_STEPS, (name, i, res["raw_path"][i])   # the step-function DP ran
         hc = M.home_const(homes[r["name"]])
         u, wh, w = _thermal_cost(r, res["fc"], i, res["S"])
         P = hc.Ph if r["season"] == "winter" else hc.Pc

@@ -218,6 +218,7 @@ def test_waves_per_home_bit_identical(gpu):
     import math
     import os
     import torch
+    from dragg_amd import _lib as L
     from dragg_amd.aggregator import DeviceAggregator
     from dragg_amd.community import synthetic_homes, synthetic_weather
     steps, dt, hh = 12, 4, 12
@@ -228,6 +229,7 @@ def test_waves_per_home_bit_identical(gpu):
     try:
         for nw in ("1", "2", "4"):
             os.environ["DRAGG_WAVES_PER_HOME"] = nw
+            L.reload_knobs()                 # (read at library load, never per step)
             agg = DeviceAggregator(homes, oat, ghi, tou, 0, steps, reward_price=[0.0], seed=12)
             for t in range(steps):
                 agg.run_iteration()
@@ -236,6 +238,7 @@ def test_waves_per_home_bit_identical(gpu):
                        agg.batch.obj.nan_to_num(7.5).cpu())
     finally:
         os.environ.pop("DRAGG_WAVES_PER_HOME", None)
+        L.reload_knobs()
     for nw in ("2", "4"):
         for a, b in zip(out["1"], out[nw]):
             assert torch.equal(a, b), nw
