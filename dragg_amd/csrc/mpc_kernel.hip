@@ -3181,6 +3181,8 @@ DEV int block_excl_max(int v, int* red, int tid) {      // max over the threads 
     return ex;
 }
 
+template <int V> struct IntC { static constexpr int value = V; };
+
 struct StepBufs {
     double *PB, *PV;              // global [POOL_CAP]: breakpoints / values of V_k, stage after stage
     int *GIA, *GIB;               // global [MC_CAP]: a stage's point ids (u << 24 | i), ping-pong, past the LDS pool
@@ -3201,18 +3203,18 @@ struct StepBufs {
 
 // exclusive prefix sums over the NT threads of the block of v[0..n) (n <= STEP_MAXU), in place
 // (xr: >= NT / 64 * STEP_MAXU ints of LDS, the caller's alone until a later barrier); one barrier
-template <int NT>
+template <int NT, int MU = STEP_MAXU>
 DEV void block_excl_scan_vec(int* v, int n, int* xr, int tid) {
     const int lane = tid & (WAVE - 1), w = tid / WAVE;
-    int inc[STEP_MAXU];
+    int inc[MU];
 #pragma unroll
-    for (int j = 0; j < STEP_MAXU; ++j) inc[j] = j < n ? dpp_iscan(v[j], lane, 0, [](int a, int b) { return a + b; }) : 0;
+    for (int j = 0; j < MU; ++j) inc[j] = j < n ? dpp_iscan(v[j], lane, 0, [](int a, int b) { return a + b; }) : 0;
     if (lane == WAVE - 1)
 #pragma unroll
-        for (int j = 0; j < STEP_MAXU; ++j) if (j < n) xr[w * STEP_MAXU + j] = inc[j];
+        for (int j = 0; j < MU; ++j) if (j < n) xr[w * STEP_MAXU + j] = inc[j];
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < STEP_MAXU; ++j) {
+    for (int j = 0; j < MU; ++j) {
         if (j >= n) continue;
         int off = 0;
         for (int i = 0; i < w; ++i) off += xr[i * STEP_MAXU + j];
@@ -3503,7 +3505,8 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         // interval of the list's last point at or before it (running per-list counts, their chunk
         // offsets by one block scan), pruned by L_k -- and the compaction of the intervals of [dl, dh].
         int res = 1, tot = 0;
-        auto stage = [&](const auto* Bk, const auto* Vk, auto* I0, auto* I1) {
+        auto stage = [&](const auto* Bk, const auto* Vk, auto* I0, auto* I1, auto mu) {
+            constexpr int MU = decltype(mu)::value;       // lists in registers in the values pass (>= NU)
             auto P = [&](int u, int i) { return (Bk[i] - g * (double)u - C) * iA; };
             auto uof = [](int id) { return id >> 24; };
             auto key = [&](int id) { return P(uof(id), id & 0xFFFFFF); };
@@ -3566,19 +3569,19 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             auto dec = [&](int c) -> double { return c < 0 ? INFINITY : fma(q, (double)(c >> 24), Vk[c & 0xFFFFFF]); };
             const int per = (Mc + NT - 1) / NT;
             const int p0 = min(Mc, tid * per), p1 = min(Mc, p0 + per);
-            int cnt[STEP_MAXU];
+            int cnt[MU];
 #pragma unroll
-            for (int j = 0; j < STEP_MAXU; ++j) cnt[j] = 0;
+            for (int j = 0; j < MU; ++j) cnt[j] = 0;
             for (int p = p0; p < p1; ++p) {
                 const int u = uof(Is[p]);
 #pragma unroll
-                for (int j = 0; j < STEP_MAXU; ++j) cnt[j] += (j == u) ? 1 : 0;
+                for (int j = 0; j < MU; ++j) cnt[j] += (j == u) ? 1 : 0;
             }
-            block_excl_scan_vec<NT>(cnt, NU, Sb.xr, tid);     // points of each list before the chunk
-            double cur[STEP_MAXU];
-            int cc[STEP_MAXU];
+            block_excl_scan_vec<NT, MU>(cnt, NU, Sb.xr, tid);     // points of each list before the chunk
+            double cur[MU];
+            int cc[MU];
 #pragma unroll
-            for (int j = 0; j < STEP_MAXU; ++j) {
+            for (int j = 0; j < MU; ++j) {
                 const int idx = Sb.rng[j] + cnt[j] - 1;   // (j < NU: rng is defined)
                 const bool ok = j < NU && cnt[j] >= 1 && idx < m;
                 cur[j] = ok ? fma(q, (double)j, Vk[idx]) : INFINITY;
@@ -3590,7 +3593,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
                 double best = INFINITY;
                 int bc = -1;
 #pragma unroll
-                for (int j = 0; j < STEP_MAXU; ++j) {
+                for (int j = 0; j < MU; ++j) {
                     if (j == u) { cur[j] = v; cc[j] = i < m ? id : -1; }
                     if (cur[j] < best) { best = cur[j]; bc = cc[j]; }
                 }
@@ -3679,14 +3682,17 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             for (int i = tid; i < m; i += NT) vs[i] = Vg[i];
         }
         SPM(24);
-        if (lds_m) {
+        // (S <= 7, every tariff of the reference: 8 lists in registers; more: the workspace path)
+        if (NU > 8) {
+            stage(Bg, Vg, Sb.GIA, Sb.GIB, IntC<STEP_MAXU>{});
+        } else if (lds_m) {
             int* const i0 = reinterpret_cast<int*>(Sb.sp + ((8 * (lds_v ? 2 : 1) * np + 15) & ~15));
-            if (lds_v) stage(bs, bs + np, i0, i0 + Mc);
-            else stage(bs, Vg, i0, i0 + Mc);
+            if (lds_v) stage(bs, bs + np, i0, i0 + Mc, IntC<8>{});
+            else stage(bs, Vg, i0, i0 + Mc, IntC<8>{});
         } else if (staged) {
-            stage(bs, Vg, Sb.GIA, Sb.GIB);
+            stage(bs, Vg, Sb.GIA, Sb.GIB, IntC<8>{});
         } else {
-            stage(Bg, Vg, Sb.GIA, Sb.GIB);
+            stage(Bg, Vg, Sb.GIA, Sb.GIB, IntC<8>{});
         }
         if (res != 1) return res;
         double* const OB = Sb.PB + top;
