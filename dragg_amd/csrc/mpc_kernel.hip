@@ -51,7 +51,7 @@ constexpr int NP_CAP = 32768;             // breakpoints of one V_k
 constexpr int POOL_CAP = 1 << 20;         // breakpoints of all V_k of one chain (the pool)
 constexpr int STEP_MAXU = 16;             // duty values 0..S (S <= 15)
 constexpr int MC_CAP = 8 * NP_CAP;        // merged candidate points of one stage ((S + 1) np, S <= 7)
-constexpr int STEP_CH = 8;                // breakpoints of one list per merge work item
+constexpr int STEP_CH = 8;                // merged outputs per merge work item, at most (fewer on small stages)
 constexpr int LW_ROWS = 256;              // rows of the LP bounds L_k / W_k per slot (H < LW_ROWS)
 constexpr int NF_MID = 384;              // front capacity of the mid launch (DM_MID)
 constexpr int NTB_MID = 128;             // ... and its key / cost buckets per stage
@@ -3519,23 +3519,25 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             }
             __syncthreads();
             auto* Is = I0; auto* Id = I1;
+            // outputs per work item: about one item per thread (a shorter walk after each co-rank search)
+            const int CHm = min(STEP_CH, max(2, (Mc + NT - 1) / NT));
             for (int w = 1; w < NU; w *= 2) {             // runs of w lists -> runs of 2w lists
                 const int npair = (NU + 2 * w - 1) / (2 * w);
                 int nseg = 0;
                 for (int pp = 0; pp < npair; ++pp) {
                     const int o0 = ro(pp * 2 * w), o2 = ro(min(NU, (pp + 1) * 2 * w));
-                    nseg += (o2 - o0 + STEP_CH - 1) / STEP_CH;
+                    nseg += (o2 - o0 + CHm - 1) / CHm;
                 }
                 for (int it = tid; it < nseg; it += NT) {
                     int pp = 0, r = it, o0 = 0, o1 = 0, o2 = 0;
                     for (; pp < npair; ++pp) {
                         o0 = ro(pp * 2 * w); o1 = ro(min(NU, pp * 2 * w + w)); o2 = ro(min(NU, (pp + 1) * 2 * w));
-                        const int ns = (o2 - o0 + STEP_CH - 1) / STEP_CH;
+                        const int ns = (o2 - o0 + CHm - 1) / CHm;
                         if (r < ns) break;
                         r -= ns;
                     }
                     const int la = o1 - o0, lb = o2 - o1;
-                    const int d0 = r * STEP_CH, d1 = min(d0 + STEP_CH, la + lb);
+                    const int d0 = r * CHm, d1 = min(d0 + CHm, la + lb);
                     // co-rank: the A points among the first d0 outputs
                     int lo_ = max(0, d0 - lb), hi_ = min(d0, la);
                     while (lo_ < hi_) {
