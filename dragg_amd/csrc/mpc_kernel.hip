@@ -3468,32 +3468,38 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         // arrays -- LDS or the workspace -- so that LDS accesses compile to ds_ loads.)
         auto ranges = [&](const auto* Bk) {
             auto P = [&](int u, int i) { return (Bk[i] - g * (double)u - C) * iA; };
-            if (tid < NU) {
-                const int u = tid;
-                int le = 0, lt = 0;                       // points <= dl, points < dh
-                for (int st = top2; st > 0; st >>= 1) {
-                    if (le + st <= np && P(u, le + st - 1) <= dl) le += st;
-                    if (lt + st <= np && P(u, lt + st - 1) < dh) lt += st;
+            if (wid == 0) {                               // (NU <= STEP_MAXU < 64: one wave)
+                const int u = lane;
+                int ilo = 0, ihi = 0, first = 0;
+                if (u < NU) {
+                    int le = 0, lt = 0;                   // points <= dl, points < dh
+                    for (int st = top2; st > 0; st >>= 1) {
+                        if (le + st <= np && P(u, le + st - 1) <= dl) le += st;
+                        if (lt + st <= np && P(u, lt + st - 1) < dh) lt += st;
+                    }
+                    ilo = max(0, le - 1);
+                    ihi = max(lt, ilo);
+                    first = (le >= 1 && ilo < ihi) ? 1 : 0;   // its first point is <= dl
                 }
-                const int ilo = max(0, le - 1), ihi = max(lt, ilo);
-                Sb.rng[u] = ilo;
-                Sb.rng[STEP_MAXU + u] = ihi;
-                Sb.rng[2 * STEP_MAXU + u] = (le >= 1 && ilo < ihi) ? 1 : 0;   // its first point is <= dl
+                // run offsets ro(u) = points of the lists before u, and the totals, by wave scans
+                const int len = ihi - ilo;
+                const int inc = dpp_iscan(len, lane, 0, [](int a_, int b_) { return a_ + b_; });
+                const int jls = dpp_iscan(first, lane, 0, [](int a_, int b_) { return a_ + b_; });
+                const int all = __shfl(inc, NU - 1), jall = __shfl(jls, NU - 1);
+                if (u < NU) {
+                    Sb.rng[u] = ilo;
+                    Sb.rng[STEP_MAXU + u] = ihi;
+                    Sb.rng[2 * STEP_MAXU + u] = first;
+                    Sb.rng[3 * STEP_MAXU + u] = inc - len;
+                } else if (u <= STEP_MAXU) {
+                    Sb.rng[3 * STEP_MAXU + u] = all;
+                }
+                if (lane == 0) Sb.rng[4 * STEP_MAXU + 1] = jall;
             }
         };
         if (staged) ranges(bs); else ranges(Bg);
         __syncthreads();
-        if (tid == 0) {                                   // run offsets ro(u) = points of the lists before u
-            int o = 0;
-            for (int u = 0; u < NU; ++u) { Sb.rng[3 * STEP_MAXU + u] = o; o += Sb.rng[STEP_MAXU + u] - Sb.rng[u]; }
-            for (int u = NU; u <= STEP_MAXU; ++u) Sb.rng[3 * STEP_MAXU + u] = o;
-        }
-        __syncthreads();
-        int Mc = 0, jl = 0;
-        for (int u = 0; u < NU; ++u) {
-            Mc += Sb.rng[STEP_MAXU + u] - Sb.rng[u];
-            jl += Sb.rng[2 * STEP_MAXU + u];
-        }
+        const int Mc = Sb.rng[3 * STEP_MAXU + STEP_MAXU], jl = Sb.rng[4 * STEP_MAXU + 1];
         if (Mc > MC_CAP) return -3;
         // run offsets: list u's points at [ro(u), ro(u + 1)) of the merge buffers
         auto ro = [&](int u) { return Sb.rng[3 * STEP_MAXU + min(u, STEP_MAXU)]; };
