@@ -3445,8 +3445,13 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         // the LDS pool: V_{k+1} (B, V) when it fits, then the merge buffers when they fit too
         double* const bs = reinterpret_cast<double*>(Sb.sp);
         const bool staged = 8 * np <= Sb.spb;
+        // V_{k+1}'s values too when they fit (both loads in flight together; first read after the merge)
+        const bool lds_v = staged && 16 * np + 32 <= Sb.spb;
         if (staged)
-            for (int i = tid; i < np; i += NT) bs[i] = Bg[i];
+            for (int i = tid; i < np; i += NT) {
+                bs[i] = Bg[i];
+                if (lds_v && i < m) bs[np + i] = Vg[i];
+            }
         // the cost pruning's L_k as an LDS table (wave 0), its minimiser and minimum
         const bool prune = U < INFINITY && Sb.lc[k] >= 1;
         if (prune && wid == 0) {
@@ -3683,12 +3688,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         };
         // the pool: V_{k+1}'s breakpoints (and values when they fit too), then the merge buffers when
         // they fit as well (ids i32 x 2; the free one then holds the values' codes)
-        const bool lds_v = staged && 16 * np + 32 <= Sb.spb;
         const bool lds_m = staged && 8 * (lds_v ? 2 : 1) * np + 8 * Mc + 32 <= Sb.spb;
-        if (lds_v) {
-            double* const vs = bs + np;
-            for (int i = tid; i < m; i += NT) vs[i] = Vg[i];
-        }
         SPM(24);
         // (S <= 7, every tariff of the reference: 8 lists in registers; more: the workspace path)
         if (NU > 8) {
