@@ -4085,7 +4085,13 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 // prices without a usable bound, a front past the big launch's capacity, S != 6): the
                 // exact step-function DP of DM_NARROW solves it, with the bucketed schedule's cost as
                 // its bound (BK_OK) -- or, where the bucketed DP found none, decides that no schedule exists
-                if (r2 < 0) {
+                // Exception (measured): an RL-priced chain past the big launch's 2,048 labels keeps its bucketed
+                // schedule unless DRAGG_FLAG_EXACT is set -- under a price that changes at every stage the
+                // step-function DP's value functions explode (the bench's smooth-price action: 776 ms with
+                // it against 30 ms without); int_path records the chain (reason 3)
+                if (MODE == DM_BUCKET && r2 == -3 && rl_prices && ok && !(a.d.flags & DRAGG_FLAG_EXACT)) {
+                    int_path |= (1 << chain) | (3 << (4 + 4 * chain));
+                } else if (r2 < 0) {
                     if (lane == 0) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30) | BK_DONE | (ok ? BK_OK : 0);
                     return;
                 }

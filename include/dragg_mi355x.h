@@ -135,10 +135,12 @@ typedef struct dragg_mpc_dims {
 
 /* dims.flags */
 enum dragg_flag {
-    /* Accepted for compatibility with ABI v6 and without effect since v7: int_mode round is exact
-       on every chain by default -- a chain the Pareto-front DPs cannot take (a feasible set
-       narrower than one duty step, mixed-sign prices without a usable bound, a front past 2,048
-       labels, S != 6) is solved by the exact step-function DP (out.int_path bit 15). */
+    /* int_mode round is exact on every TOU chain by default: a chain the Pareto-front DPs cannot
+       take (a feasible set narrower than one duty step, mixed-sign prices without a usable bound, a
+       front past 2,048 labels, S != 6) is solved by the exact step-function DP (out.int_path bit
+       15).  The one exception: a chain under RL prices (a price change at more than H/4 stages)
+       whose front passes 2,048 labels keeps its bucketed schedule (int_path reason 3) unless this
+       flag is set -- there the step-function DP costs ~25x the whole RL action. */
     DRAGG_FLAG_EXACT = 1
 };
 

