@@ -163,7 +163,6 @@ class DeviceAggregator:
                  "hist": self.hist[:t].cpu() if self.hist is not None else None}
         tmp = path + ".tmp"
         torch.save(state, tmp)
-        import os
         os.replace(tmp, path)                 # a crash mid-write leaves the previous checkpoint
         return path
 
@@ -202,8 +201,8 @@ class DeviceAggregator:
         if path is not None and os.path.isfile(path):
             try:
                 t = self.load_state(path)
-            except (ValueError, KeyError, RuntimeError, OSError, EOFError) as e:
-                err, t = e, -1
+            except Exception as e:      # any refusal (incl. pickle.UnpicklingError from a garbage
+                err, t = e, -1          # file under weights_only=True) must reach the collective
         try:
             t = self.agree(t, "the checkpoint timestep to resume from")
         except RuntimeError as e:

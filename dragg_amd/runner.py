@@ -244,7 +244,8 @@ class Aggregator:
     def run_rl_agg(self, policy, noise_fn=None):
         """The `run_rl_agg` case (README.md:55): MPC homes under an RL-designed reward price.
         `policy(aggregator) -> reward price` is called once per timestep (e.g. an
-        `dragg_amd.rl.RLAgent`'s `act`); it may call `rl_forecast` to try candidate prices.
+        `dragg_amd.rl.SetpointAgent.act`, or the reference's agent via `rl.policy_from_agent`);
+        it may call `rl_forecast` to try candidate prices.
         Writes `<run dir>/rl_agg/results.json` with the Summary's RP and p_grid_setpoint."""
         self.case = "rl_agg"
         self.get_homes()

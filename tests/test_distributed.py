@@ -249,6 +249,19 @@ def _resume_worker(rank, world, port, root, q):
         out["foreign"] = "own: " + str(ex)
     except RuntimeError as ex:
         out["foreign"] = str(ex)
+    # rank 0's checkpoint file is garbage (torch.load(weights_only=True) raises
+    # pickle.UnpicklingError): rank 0 raises that, rank 1 the disagreement -- neither hangs
+    junk = os.path.join(root, f"junk-{rank}.pt")
+    with open(junk, "wb") as f:
+        f.write(b"not a checkpoint" if rank == 0 else open(path, "rb").read())
+    g = DeviceAggregator(homes, [0.0], [0.0], [0.0], **kw)
+    try:
+        g.resume(junk)
+        out["garbage"] = "ok"
+    except RuntimeError as ex:
+        out["garbage"] = str(ex)
+    except Exception as ex:
+        out["garbage"] = "own: " + type(ex).__name__
     # a crashing home on rank 1 only: both ranks raise the same KeyError together
     kw["batch_cls"] = ErrBatch
     d = DeviceAggregator(homes, [0.0], [0.0], [0.0], **kw)
@@ -278,3 +291,5 @@ def test_two_ranks_resume_disagreement_and_errors_raise_on_every_rank(tmp_path):
         assert "home h3 at timestep 2" in res[rank]["err"]
     assert res[1]["foreign"].startswith("own: ") and "another run" in res[1]["foreign"]
     assert "ranks disagree" in res[0]["foreign"]
+    assert res[0]["garbage"] == "own: UnpicklingError", res[0]["garbage"]
+    assert "ranks disagree" in res[1]["garbage"]

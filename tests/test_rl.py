@@ -1,8 +1,9 @@
-"""RL reward-price path: host agent (agent.py:42-282), the aggregator's RL
+"""RL reward-price path: host policies (this build's PI controller and the
+hook for the reference's agent, agent.py:130-149), the aggregator's RL
 hooks (aggregator.py:664-696, 876-911) and the device-side pieces the agent drives -- the
 reward-price broadcast and forecast rollouts that re-solve every home without committing.
 
-CPU: the agent's arithmetic, the setpoint recursion, the rollout snapshot/restore and the
+CPU: the policies, the setpoint recursion, the rollout snapshot/restore and the
 two-rank price broadcast + rollout all-reduce (gloo, stand-in solver).
 GPU: a rollout equals the committed step it forecasts, bit for bit, and leaves the state
 untouched; an RL run under a constant price equals a direct run with that price."""
@@ -16,72 +17,57 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from dragg_amd.aggregator import DeviceAggregator
-from dragg_amd.rl import RLAgent, SetpointAgent, ridge_fit
+from dragg_amd.rl import SetpointAgent, policy_from_agent
 from tests.test_distributed import _free_port
 
 
-# ------------------------------------------------------------------ agent (host)
-def test_ridge_fit_matches_sklearn():
-    from sklearn.linear_model import Ridge
-    rng = np.random.default_rng(0)
-    X = rng.normal(size=(12, 71))
-    y = rng.normal(size=12)
-    ref = Ridge(alpha=0.01).fit(X, y).coef_
-    np.testing.assert_allclose(ridge_fit(X, y, 0.01), ref, rtol=1e-7, atol=1e-9)
-
-
-def test_basis_sizes_and_terms():
-    s = {"fcst_error": 0.5, "forecast_trend": -2.0, "time_of_day": 0.25, "delta_action": 3.0}
-    phi = RLAgent.state_basis(s)
-    assert phi.shape == (23,)                 # (3*3-1)*3 - 1
-    # (f, f², e, ...) ⊗ (1, sin, cos) without the leading f*1: f*sin, f*cos, f², ...
-    assert phi[0] == pytest.approx(-2.0) and phi[1] == pytest.approx(0.0, abs=1e-15) and phi[2] == 4.0
-    xu = RLAgent.state_action_basis(s, 1.5)
-    assert xu.shape == (3 * 24 - 1,)
-
-
+# ------------------------------------------------------------------ policies (host)
 CFG = {"rl": {"utility": {"action_space": [-5, 5], "action_scale": 100}}}
-PARAMS = {"alpha": 0.05, "beta": 0.9, "batch_size": 4, "twin_q": False, "epsilon": 0.1}
 
 
 class _Env:
     def __init__(self):
-        self.agg_setpoint, self.forecast_load, self.prev_forecast_load = 10.0, 12.0, 11.0
-        self.timestep, self.dt = 0, 4
+        self.agg_setpoint, self.forecast_load = 10.0, 12.0
 
 
-def test_agent_trains_and_replays():
-    import random
-    random.seed(0)
-    ag = SetpointAgent(PARAMS, CFG, rng=np.random.RandomState(1))
+def test_setpoint_agent_pi_control():
+    """This build's PI policy: above the setpoint the price rises, the integral is clamped
+    (anti-windup) and every price lies within action_space / action_scale."""
+    ag = SetpointAgent(CFG, kp=1.0, ki=0.5)
     env = _Env()
-    prices = []
-    for t in range(12):
-        env.timestep = t
-        env.forecast_load = 10.0 + np.sin(t)
-        prices.append(ag.act(env))
-    assert len(ag.memory) > PARAMS["batch_size"]          # the ridge replay ran
-    assert all(abs(p) <= 0.05 for p in prices)            # clipped to the action space / scale
-    assert np.all(np.isfinite(ag.theta_q)) and np.all(np.isfinite(ag.theta_mu))
-    assert len(ag.rl_data["reward"]) == 12
-
-
-def test_twin_q_raises_like_reference():
-    """agent.py:204 assigns a 2n-long flatten() into an n-long column: numpy raises."""
-    import random
-    random.seed(0)
-    ag = SetpointAgent(dict(PARAMS, twin_q=True), CFG, rng=np.random.RandomState(1))
-    env = _Env()
-    with pytest.raises(ValueError):
-        for t in range(12):
-            env.timestep = t
-            env.forecast_load = 10.0 + np.sin(t)
-            ag.act(env)
+    p1 = ag.act(env)                                     # e = 0.2: 0.2 + 0.5 * 0.2
+    assert p1 == pytest.approx(0.3 / 100)
+    env.forecast_load = 1000.0                           # e = 99: saturates
+    prices = [ag.act(env) for _ in range(20)]
+    assert all(p == pytest.approx(0.05) for p in prices)
+    assert ag.integral == pytest.approx(5 / 0.5)         # clamped, not 20 * 99
+    env.forecast_load = 10.0                             # e = 0: only the (clamped) integral term remains
+    assert ag.act(env) == pytest.approx(0.05)
+    env.forecast_load = 0.0                              # e = -1
+    assert ag.act(env) < 0.05
+    assert len(ag.history["action"]) == 23
 
 
 def test_missing_action_space_raises():
     with pytest.raises(KeyError):
-        SetpointAgent(PARAMS, {"rl": {"utility": {}}})
+        SetpointAgent({"rl": {"utility": {}}})
+
+
+def test_reference_agent_plugs_in():
+    """A reference-style agent (train(env) -> action, agent.py:130-149) becomes the policy
+    run_rl_agg calls; it sees the aggregator as its env."""
+    class Agent:
+        def __init__(self):
+            self.seen = []
+
+        def train(self, env):
+            self.seen.append(env.forecast_load)
+            return 2.0 * len(self.seen)
+
+    ag = Agent()
+    pol = policy_from_agent(ag, scale=100.0)
+    env = _Env()
+    assert pol(env) == 0.02 and pol(env) == 0.04 and ag.seen == [12.0, 12.0]
 
 
 # ------------------------------------------------------------------ setpoint (host)
