@@ -74,6 +74,11 @@ def parse(argv=None):
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic: time rank 0's strided shard of the community sharded this many ways, on "
                          "one GPU without the collectives (the per-GPU load of an N-GPU strong-scaling run)")
+    ap.add_argument("--shard-rank", type=int, default=0,
+                    help="with --shard-of N: which rank's shard to time (0..N-1)")
+    ap.add_argument("--shard-max", action="store_true",
+                    help="with --shard-of N: time EVERY rank's shard in turn (same steps each) and report the "
+                         "slowest one -- the step time of an N-GPU strong-scaling run is its slowest rank's")
     ap.add_argument("--exact", action="store_true",
                     help="DRAGG_FLAG_EXACT (diagnostic): every chain the front DPs cannot take goes to the step-function DP")
     ap.add_argument("--no-history", action="store_true",
@@ -479,12 +484,7 @@ def main():
     # keep_history: the per-step hash history (collected_data, aggregator.py:737-748) is written
     # inside the timed steps, as a configs[2] run does
     shard = args.shard_of > 1 and world == 1
-    agg = DeviceAggregator(homes, oat, ghi, tou, 0, total_steps, reward_price=[0.0],
-                           int_mode=args.int_mode, seed=12, rank=rank, world=args.shard_of if shard else world,
-                           keep_history=not args.no_history, exact=args.exact)
-    if shard:
-        agg.world = 1                     # one GPU: no collectives (the shard's own sums)
-    stream = torch.cuda.current_stream()
+    fh = args.forecast_horizon if rl else 0
 
     def barrier():
         torch.cuda.synchronize()
@@ -492,37 +492,64 @@ def main():
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
-    fh = args.forecast_horizon if rl else 0
+    def timed(shard_rank):
+        """Build the aggregator (this rank's shard, or shard `shard_rank` of --shard-of on one GPU),
+        run the warmup steps, then time exactly --steps steps between barriers."""
+        agg = DeviceAggregator(homes, oat, ghi, tou, 0, total_steps, reward_price=[0.0],
+                               int_mode=args.int_mode, seed=12, rank=shard_rank if shard else rank,
+                               world=args.shard_of if shard else world,
+                               keep_history=not args.no_history, exact=args.exact)
+        if shard:
+            agg.world = 1                     # one GPU: no collectives (the shard's own sums)
+        stream = torch.cuda.current_stream()
 
-    def action(k):
-        """rl: one reward-price action (random stand-in for the host agent's choice)."""
-        agg.set_reward_price(prices[k])
-        agg.forecast(fh)
+        def action(k):
+            """rl: one reward-price action (random stand-in for the host agent's choice)."""
+            agg.set_reward_price(prices[k])
+            agg.forecast(fh)
 
-    for k in range(args.warmup):
-        if rl:
-            action(k)
-        agg.run_iteration()
-        agg.collect_data(defer=not rl)
-    if not rl:
-        agg.reduce_history()
-    barrier()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        evs[k][0].record(stream)            # rl: the action's rollout solves are timed with its step
-        if rl:
-            action(args.warmup + k)
-        agg.run_iteration()
-        evs[k][1].record(stream)
-        if rl:
-            agg.collect_data().tolist()         # the agent reads the community sums on the host
-        else:
-            agg.collect_data(defer=True)        # run_rbo_mpc: no feedback, one reduction at the end
-    if not rl:
-        agg.reduce_history()
-    barrier()
-    elapsed = time.perf_counter() - t0
+        for k in range(args.warmup):
+            if rl:
+                action(k)
+            agg.run_iteration()
+            agg.collect_data(defer=not rl)
+        if not rl:
+            agg.reduce_history()
+        barrier()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            evs[k][0].record(stream)            # rl: the action's rollout solves are timed with its step
+            if rl:
+                action(args.warmup + k)
+            agg.run_iteration()
+            evs[k][1].record(stream)
+            if rl:
+                agg.collect_data().tolist()         # the agent reads the community sums on the host
+            else:
+                agg.collect_data(defer=True)        # run_rbo_mpc: no feedback, one reduction at the end
+        if not rl:
+            agg.reduce_history()
+        barrier()
+        return agg, time.perf_counter() - t0, evs
+
+    shard_times = None
+    if shard and args.shard_max:
+        # every shard in turn; the slowest one is what an N-GPU run waits for (its aggregator is kept)
+        runs = []
+        for r in range(args.shard_of):
+            agg, el, evs = timed(r)
+            runs.append((el, r))
+            if el >= max(x[0] for x in runs):
+                keep = (agg, el, evs, r)
+            del agg
+            torch.cuda.empty_cache()
+        agg, elapsed, evs, slow_rank = keep
+        shard_times = {"ms_per_step": [round(el / args.steps * 1e3, 4) for el, _ in sorted(runs, key=lambda x: x[1])],
+                       "slowest_rank": slow_rank}
+    else:
+        slow_rank = args.shard_rank if shard else rank
+        agg, elapsed, evs = timed(slow_rank)
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
@@ -582,10 +609,14 @@ def main():
                        "global_batch": n_total,
                        "horizon": H, "mix": "40/20/20/20 base/pv/battery/pv_battery",
                        "parallelism": f"homes sharded x{world}"},
-            "shard_emulation": ({"shard_of": args.shard_of, "homes": agg.batch.N,
-                                 "note": "diagnostic: rank 0's strided shard alone on one GPU (the per-GPU load of "
-                                         "an N-GPU strong-scaling run), no collectives; value counts the shard's "
-                                         "solves"} if shard else None),
+            "shard_emulation": ({"shard_of": args.shard_of, "shard_rank": slow_rank, "homes": agg.batch.N,
+                                 "max_over_shards": shard_times,
+                                 "note": ("diagnostic: EVERY rank's strided shard in turn on one GPU, no collectives; "
+                                          "the line is the slowest shard's (an N-GPU strong-scaling step waits for its "
+                                          "slowest rank); value counts that shard's solves" if shard_times else
+                                          f"diagnostic: rank {slow_rank}'s strided shard alone on one GPU (the per-GPU "
+                                          "load of an N-GPU strong-scaling run), no collectives; value counts the "
+                                          "shard's solves")} if shard else None),
             "window": window(args.warmup, args.steps, dt, args.month, rl),
             "history_written": not args.no_history,
             "sim_wall_s": elapsed,

@@ -1,0 +1,45 @@
+#!/bin/bash
+# Round-5 session: selected GPU tests (TESTS, "none" to skip), bench lines (LINES), optional
+# kernel trace of one line (TRACE=<line name>).  Each step under its own limit; results under
+# gpurun_out/$TAG.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+OUT=gpurun_out/${TAG:-r05}
+mkdir -p $OUT
+( while sleep 60; do echo "tick $(date +%T)" >> $OUT/heartbeat; done ) &
+HB=$!
+trap "kill $HB" EXIT
+export TMPDIR=/tmp
+TESTS=${TESTS:-tests}
+if [ "$TESTS" != "none" ]; then
+  timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest $TESTS -m gpu -x -v -s --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest.log; exit 1; }
+  tail -2 $OUT/pytest.log
+fi
+args_of() {
+  case $1 in
+    driver) echo --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 ;;
+    full96) echo --steps 96 --warmup 4 --cpu-seconds 0 ;;
+    exact96) echo --steps 96 --warmup 4 --cpu-seconds 0 --exact ;;
+    shard8) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 ;;
+    shard8max) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 --shard-max ;;
+    shard4max) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 4 --shard-max ;;
+    shard2max) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 2 --shard-max ;;
+    rl) echo --workload rl --steps 6 --warmup 1 --cpu-seconds 0 ;;
+    cfg1) echo --homes 1000 --horizon-hours 6 --month 1 --steps 96 --warmup 4 --cpu-seconds 0 ;;
+    h24) echo --horizon-hours 6 --steps 96 --warmup 4 --cpu-seconds 0 ;;
+    cfg3) echo --homes 100000 --horizon-hours 6 --steps 24 --warmup 2 --cpu-seconds 0 ;;
+    gloo2) echo --gpus 2 --steps 20 --warmup 5 --cpu-seconds 0 ;;
+  esac
+}
+run() { name=$1
+  if [ $name = gloo2 ]; then export DRAGG_BENCH_BACKEND=gloo; else unset DRAGG_BENCH_BACKEND; fi
+  timeout -k 10 ${LINE_LIMIT:-400} python3 bench.py $(args_of $name) > $OUT/$name.out 2> $OUT/$name.err || { echo "$name failed"; tail -5 $OUT/$name.err; exit 1; }
+  grep '^{' $OUT/$name.out | tail -1 > $OUT/$name.json
+  python3 -c "
+import json; d=json.load(open('$OUT/$name.json')); print('$name', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],4), 'ms/step', 'kern', round(d['roofline']['kernel_ms'],4), (d.get('shard_emulation') or {}).get('max_over_shards'), {k: v for k, v in d['status_counts'].items() if v and k != 'optimal'})"; }
+for spec in ${LINES:-full96}; do run $spec; done
+if [ -n "$TRACE" ]; then
+  timeout -k 10 ${LINE_LIMIT:-400} rocprofv3 --kernel-trace --stats -d $OUT/trace_$TRACE -o run -- python3 bench.py $(args_of $TRACE) > $OUT/trace_$TRACE.log 2>&1 || { echo "trace failed"; tail -5 $OUT/trace_$TRACE.log; exit 1; }
+  f=$(find $OUT/trace_$TRACE -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && head -8 "$f"
+fi
+echo session-done
