@@ -51,6 +51,7 @@ constexpr int NP_CAP = 32768;             // breakpoints of one V_k
 constexpr int POOL_CAP = 1 << 20;         // breakpoints of all V_k of one chain (the pool)
 constexpr int STEP_MAXU = 16;             // duty values 0..S (S <= 15)
 constexpr int MC_CAP = 8 * NP_CAP;        // merged candidate points of one stage ((S + 1) np, S <= 7)
+constexpr int STEP_CH = 8;                // merged outputs per merge work item, at most (fewer on small stages)
 constexpr int LW_ROWS = 256;              // rows of the LP bounds L_k / W_k per slot (H < LW_ROWS)
 constexpr int NF_MID = 384;              // front capacity of the mid launch (DM_MID)
 constexpr int NTB_MID = 128;             // ... and its key / cost buckets per stage
@@ -1578,7 +1579,7 @@ __host__ __device__ inline int direct_lds_bytes(int H, int S) { return direct_la
 // [H + 1] i32, scan scratch, list ranges, the reachable hull and the cut domains [H + 1] f64, the
 // recovery's duty values, L_k's table, then a pool with the rest of the CU's LDS: per stage V_{k+1}
 // (B, V) and the merge buffers (keys f64 x 2, ids i32 x 2) where they fit
-struct NarrowLayout { int off, cnt, wc, lc, red, xr, rng, rl, rh, dlo, dhi, xv, lt, rk, sp, spb, bytes; };
+struct NarrowLayout { int off, cnt, wc, lc, red, xr, rng, rl, rh, dlo, dhi, xv, lt, sp, spb, bytes; };
 __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
     NarrowLayout o{};
     int p = direct_layout(H, S).bytes;
@@ -1596,7 +1597,6 @@ __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
     o.dhi = take(8 * (H + 1), 8);
     o.xv = take(8 * STEP_MAXU, 8);
     o.lt = take(8 * (3 * WAVE + 2), 16);
-    o.rk = take(8 * 2 * STEP_MAXU, 8);
     // the pool takes what is left of the CU's LDS (>= the waves' PL tables of lp_cut)
     o.sp = take(0, 16);
     o.spb = max(NT_STEPS / 64 * 6 * WAVE * 8, ((160 * 1024 - 256) - o.sp - 64) / 64 * 64);
@@ -3197,7 +3197,6 @@ struct StepBufs {
     double *xv;                   // LDS [STEP_MAXU] recovery: value of each duty
     double *lt;                   // LDS [3][WAVE] + 2: L_k as a table (points, values, slopes), its
                                   //   minimiser and minimum (the cost pruning)
-    double *rk;                   // LDS [2 STEP_MAXU]: per list the first / last key of its run (+inf / -inf: empty)
     char* sp;                     // LDS pool [spb] bytes: per stage V_{k+1} (B, V) and the merge buffers
     int spb;                      //   (lp_cut: the waves' PL tables)
 };
@@ -3430,7 +3429,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
     unsigned long long sp_t = __builtin_amdgcn_s_memtime();
     auto sp_mark = [&](int slot_) {
         const unsigned long long n_ = __builtin_amdgcn_s_memtime();
-        if (tid == 0 && !feas_only) X[slot_ * 8 + S_PAD] += (double)(n_ - sp_t);
+        if (tid == 0 && !feas_only && slot_ < H) X[slot_ * 8 + S_PAD] += (double)(n_ - sp_t);
         sp_t = n_;
     };
 #define SPM(i) sp_mark(i)
@@ -3495,8 +3494,6 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
                 if (u < NU) {
                     Sb.rng[u] = ilo;
                     Sb.rng[STEP_MAXU + u] = ihi;
-                    Sb.rk[u] = ilo < ihi ? P(u, ilo) : INFINITY;
-                    Sb.rk[STEP_MAXU + u] = ilo < ihi ? P(u, ihi - 1) : -INFINITY;
                     Sb.rng[2 * STEP_MAXU + u] = first;
                     Sb.rng[3 * STEP_MAXU + u] = inc - len;
                 } else if (u <= STEP_MAXU) {
@@ -3512,74 +3509,108 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         // run offsets: list u's points at [ro(u), ro(u + 1)) of the merge buffers
         auto ro = [&](int u) { return Sb.rng[3 * STEP_MAXU + min(u, STEP_MAXU)]; };
         SPM(21);
-        // The merge of the runs (key P, id = u << 24 | i) with each merged point's value -- the value of the
-        // elementary interval it starts: min over the lists of q u + V_{k+1} on the interval of the list's
-        // last point at or before it -- in one rank pass, then the compaction of the intervals of [dl, dh]
-        // (pruned by L_k).
+        // The merge: the lists written as runs of (key P, id = u << 24 | i) into buffer 0, then pairs of
+        // adjacent runs merged level by level (merge path: every thread takes an equal segment of a
+        // pair's output, its start found by a co-rank binary search), then each merged point's value --
+        // the value of the elementary interval it starts: min over the lists of q u + V_{k+1} on the
+        // interval of the list's last point at or before it (running per-list counts, their chunk
+        // offsets by one block scan), pruned by L_k -- and the compaction of the intervals of [dl, dh].
         int res = 1, tot = 0;
         auto stage = [&](const auto* Bk, const auto* Vk, auto* I0, auto* I1, auto mu) {
             constexpr int MU = decltype(mu)::value;       // lists in registers in the values pass (>= NU)
             auto P = [&](int u, int i) { return (Bk[i] - g * (double)u - C) * iA; };
             auto uof = [](int id) { return id >> 24; };
             auto key = [&](int id) { return P(uof(id), id & 0xFFFFFF); };
-            // a value code j << 24 | idx: q j + V_{k+1}[idx], recomputed bit-identically (-1: +inf)
-            auto dec = [&](int c) -> double { return c < 0 ? INFINITY : fma(q, (double)(c >> 24), Vk[c & 0xFFFFFF]); };
-            // One pass, no merge levels: every point p = (u, i) of the runs finds its place in the merged
-            // order (key, u, i) as its index in its own run plus, per other list j, the count of j's run points
-            // before it (j < u: keys <= K; j > u: keys < K) -- a whole run before / after it by the run's
-            // first / last key, a binary search otherwise, the searches of all lists interleaved level by
-            // level -- and its interval value: min over the lists (lowest j on ties) of q j + V_{k+1} at
-            // list j's last point at or before p (the point itself for j = u).  The same order and the same
-            // codes as a pairwise merge of the runs followed by a running-count pass over them.
-            auto* const Is = I1;
-            auto* const VAL = I0;
+            // a before b in the merged order (P, u); the caller passes keys it already holds
+            auto less = [&](double ka, int ia, double kb, int ib) { return ka < kb || (ka == kb && uof(ia) < uof(ib)); };
             for (int e = tid; e < Mc; e += NT) {
                 int u = 0;
                 while (u < NU - 1 && e >= ro(u + 1)) ++u;
-                const int i = Sb.rng[u] + (e - ro(u));
-                const double K = P(u, i);
-                int lo_[MU], len_[MU];
-                bool srch[MU];
-                int stmax = 0;
-#pragma unroll
-                for (int j = 0; j < MU; ++j) {
-                    const int l = j < NU ? Sb.rng[STEP_MAXU + j] - Sb.rng[j] : 0;
-                    len_[j] = l;
-                    lo_[j] = 0;
-                    srch[j] = false;
-                    if (j >= NU || j == u || l == 0) continue;
-                    const double fk = Sb.rk[j], lk = Sb.rk[STEP_MAXU + j];
-                    if (j < u ? lk <= K : lk < K) lo_[j] = l;                  // the whole run before p
-                    else if (j < u ? fk <= K : fk < K) { srch[j] = true; stmax = max(stmax, l); }
+                I0[e] = (u << 24) | (Sb.rng[u] + (e - ro(u)));
+            }
+            __syncthreads();
+            auto* Is = I0; auto* Id = I1;
+            // outputs per work item: about one item per thread (a shorter walk after each co-rank search)
+            const int CHm = min(STEP_CH, max(2, (Mc + NT - 1) / NT));
+            for (int w = 1; w < NU; w *= 2) {             // runs of w lists -> runs of 2w lists
+                const int npair = (NU + 2 * w - 1) / (2 * w);
+                int nseg = 0;
+                for (int pp = 0; pp < npair; ++pp) {
+                    const int o0 = ro(pp * 2 * w), o2 = ro(min(NU, (pp + 1) * 2 * w));
+                    nseg += (o2 - o0 + CHm - 1) / CHm;
                 }
-                // counts by binary search: lo_ = points of list j's run before p
-                for (int st = stmax ? 1 << (31 - __builtin_clz((unsigned)stmax)) : 0; st > 0; st >>= 1) {
-#pragma unroll
-                    for (int j = 0; j < MU; ++j) {
-                        if (!srch[j] || lo_[j] + st > len_[j]) continue;
-                        const double kj = P(j, Sb.rng[j] + lo_[j] + st - 1);
-                        if (j < u ? kj <= K : kj < K) lo_[j] += st;
+                for (int it = tid; it < nseg; it += NT) {
+                    int pp = 0, r = it, o0 = 0, o1 = 0, o2 = 0;
+                    for (; pp < npair; ++pp) {
+                        o0 = ro(pp * 2 * w); o1 = ro(min(NU, pp * 2 * w + w)); o2 = ro(min(NU, (pp + 1) * 2 * w));
+                        const int ns = (o2 - o0 + CHm - 1) / CHm;
+                        if (r < ns) break;
+                        r -= ns;
+                    }
+                    const int la = o1 - o0, lb = o2 - o1;
+                    const int d0 = r * CHm, d1 = min(d0 + CHm, la + lb);
+                    // co-rank: the A points among the first d0 outputs
+                    int lo_ = max(0, d0 - lb), hi_ = min(d0, la);
+                    while (lo_ < hi_) {
+                        const int mid = (lo_ + hi_) >> 1;
+                        const int ib = Is[o1 + d0 - mid - 1], ia = Is[o0 + mid];
+                        if (less(key(ib), ib, key(ia), ia)) hi_ = mid;
+                        else lo_ = mid + 1;
+                    }
+                    int ia_ = lo_, ib_ = d0 - lo_;
+                    int xa = ia_ < la ? Is[o0 + ia_] : 0, xb = ib_ < lb ? Is[o1 + ib_] : 0;
+                    double ka = ia_ < la ? key(xa) : INFINITY, kb = ib_ < lb ? key(xb) : INFINITY;
+                    for (int d = d0; d < d1; ++d) {
+                        const bool ta = ib_ >= lb || (ia_ < la && less(ka, xa, kb, xb));
+                        Id[o0 + d] = ta ? xa : xb;
+                        if (ta) {
+                            ++ia_;
+                            if (ia_ < la) { xa = Is[o0 + ia_]; ka = key(xa); }
+                        } else {
+                            ++ib_;
+                            if (ib_ < lb) { xb = Is[o1 + ib_]; kb = key(xb); }
+                        }
                     }
                 }
-                int pos = e - ro(u);
+                __syncthreads();
+                auto* ti = Is; Is = Id; Id = ti;
+            }
+            SPM(25);
+            // values: Is holds the merged points; the free buffer receives each one's interval value as a
+            // code j << 24 | idx (the value is q j + V_{k+1}[idx], recomputed bit-identically; -1: +inf)
+            auto* const VAL = Id;
+            auto dec = [&](int c) -> double { return c < 0 ? INFINITY : fma(q, (double)(c >> 24), Vk[c & 0xFFFFFF]); };
+            const int per = (Mc + NT - 1) / NT;
+            const int p0 = min(Mc, tid * per), p1 = min(Mc, p0 + per);
+            int cnt[MU];
+#pragma unroll
+            for (int j = 0; j < MU; ++j) cnt[j] = 0;
+            for (int p = p0; p < p1; ++p) {
+                const int u = uof(Is[p]);
+#pragma unroll
+                for (int j = 0; j < MU; ++j) cnt[j] += (j == u) ? 1 : 0;
+            }
+            block_excl_scan_vec<NT, MU>(cnt, NU, Sb.xr, tid);     // points of each list before the chunk
+            double cur[MU];
+            int cc[MU];
+#pragma unroll
+            for (int j = 0; j < MU; ++j) {
+                const int idx = Sb.rng[j] + cnt[j] - 1;   // (j < NU: rng is defined)
+                const bool ok = j < NU && cnt[j] >= 1 && idx < m;
+                cur[j] = ok ? fma(q, (double)j, Vk[idx]) : INFINITY;
+                cc[j] = ok ? (j << 24) | idx : -1;
+            }
+            for (int p = p0; p < p1; ++p) {
+                const int id = Is[p], u = uof(id), i = id & 0xFFFFFF;
+                const double v = i < m ? fma(q, (double)u, Vk[i]) : INFINITY;
                 double best = INFINITY;
                 int bc = -1;
 #pragma unroll
                 for (int j = 0; j < MU; ++j) {
-                    if (j >= NU) continue;
-                    double v = INFINITY;
-                    int c = -1;
-                    if (j == u) {
-                        if (i < m) { v = fma(q, (double)u, Vk[i]); c = (u << 24) | i; }
-                    } else {
-                        pos += lo_[j];
-                        const int idx = Sb.rng[j] + lo_[j] - 1;
-                        if (lo_[j] >= 1 && idx < m) { v = fma(q, (double)j, Vk[idx]); c = (j << 24) | idx; }
-                    }
-                    if (v < best) { best = v; bc = c; }
+                    if (j == u) { cur[j] = v; cc[j] = i < m ? id : -1; }
+                    if (cur[j] < best) { best = cur[j]; bc = cc[j]; }
                 }
-                Is[pos] = (u << 24) | i;
-                VAL[pos] = bc;
+                VAL[p] = bc;
             }
             __syncthreads();
             SPM(26);
@@ -3876,7 +3907,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                                   reinterpret_cast<double*>(sb + nl.rl), reinterpret_cast<double*>(sb + nl.rh),
                                   reinterpret_cast<double*>(sb + nl.dlo), reinterpret_cast<double*>(sb + nl.dhi),
                                   reinterpret_cast<double*>(sb + nl.xv), reinterpret_cast<double*>(sb + nl.lt),
-                                  reinterpret_cast<double*>(sb + nl.rk), sb + nl.sp, nl.spb};
+                                  sb + nl.sp, nl.spb};
                 auto steps = [&](bool feas, bool cut, double U_ = INFINITY) {
                     return dp_steps<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, D.x, sx, sv, lane, feas, cut, U_);
                 };
@@ -3893,7 +3924,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 unsigned long long pt = __builtin_amdgcn_s_memtime();
                 auto pmark = [&](int slot_) {
                     const unsigned long long n_ = __builtin_amdgcn_s_memtime();
-                    if (lane == 0) D.x[slot_ * 8 + S_PAD] += (double)(n_ - pt);
+                    if (lane == 0 && slot_ < H) D.x[slot_ * 8 + S_PAD] += (double)(n_ - pt);
                     pt = n_;
                 };
                 if (lane == 0) D.x[19 * 8 + S_PAD] = ub;

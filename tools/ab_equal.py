@@ -27,6 +27,8 @@ def dump(a):
     for t in range(a.steps):
         agg.run_iteration()
         torch.cuda.synchronize()
+        if t < a.first:
+            continue
         out[f"vals{t}"] = agg.batch.vals.cpu().numpy()
         out[f"fc{t}"] = agg.batch.fc.cpu().numpy()
         out[f"st{t}"] = agg.batch.status.cpu().numpy()
@@ -66,6 +68,7 @@ if __name__ == "__main__":
     ap.add_argument("--horizon-hours", type=int, default=12)
     ap.add_argument("--month", type=int, default=7)
     ap.add_argument("--dt", type=int, default=4)
+    ap.add_argument("--first", type=int, default=0, help="dump the steps from this one on")
     a = ap.parse_args()
     if a.compare:
         sys.exit(0 if compare(*a.compare) else 1)

@@ -39,7 +39,7 @@ run() { name=$1
 import json; d=json.load(open('$OUT/$name.json')); print('$name', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],4), 'ms/step', 'kern', round(d['roofline']['kernel_ms'],4), (d.get('shard_emulation') or {}).get('max_over_shards'), {k: v for k, v in d['status_counts'].items() if v and k != 'optimal'})"; }
 for spec in ${LINES:-full96}; do run $spec; done
 if [ -n "$TRACE" ]; then
-  timeout -k 10 ${LINE_LIMIT:-400} rocprofv3 --kernel-trace --stats -d $OUT/trace_$TRACE -o run -- python3 bench.py $(args_of $TRACE) > $OUT/trace_$TRACE.log 2>&1 || { echo "trace failed"; tail -5 $OUT/trace_$TRACE.log; exit 1; }
+  timeout -k 10 ${LINE_LIMIT:-400} rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$TRACE -o run -- python3 bench.py $(args_of $TRACE) > $OUT/trace_$TRACE.log 2>&1 || { echo "trace failed"; tail -5 $OUT/trace_$TRACE.log; exit 1; }
   f=$(find $OUT/trace_$TRACE -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && head -8 "$f"
 fi
 echo session-done
