@@ -81,6 +81,8 @@ def parse(argv=None):
                          "slowest one -- the step time of an N-GPU strong-scaling run is its slowest rank's")
     ap.add_argument("--exact", action="store_true",
                     help="DRAGG_FLAG_EXACT (diagnostic): every chain the front DPs cannot take goes to the step-function DP")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="rbo: serial steps (no lag mode: every home's step t completes before step t + 1 starts)")
     ap.add_argument("--no-history", action="store_true",
                     help="skip the per-step history write (collected_data); a configs[2] run keeps it")
     ap.add_argument("--keep-crashing-homes", action="store_true",
@@ -498,7 +500,8 @@ def main():
         agg = DeviceAggregator(homes, oat, ghi, tou, 0, total_steps, reward_price=[0.0],
                                int_mode=args.int_mode, seed=12, rank=shard_rank if shard else rank,
                                world=args.shard_of if shard else world,
-                               keep_history=not args.no_history, exact=args.exact)
+                               keep_history=not args.no_history, exact=args.exact,
+                               overlap=not (rl or args.no_overlap))
         if shard:
             agg.world = 1                     # one GPU: no collectives (the shard's own sums)
         stream = torch.cuda.current_stream()
@@ -619,6 +622,7 @@ def main():
                                           "shard's solves")} if shard else None),
             "window": window(args.warmup, args.steps, dt, args.month, rl),
             "history_written": not args.no_history,
+            "lag_mode": bool(agg.overlap),
             "sim_wall_s": elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0,
@@ -631,7 +635,8 @@ def main():
                          "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_step": alg_bytes,
                          "unit_note": "one step = the hot launch + the second launch of one timestep; HIP events "
-                                      "on the launch stream around run_iteration"},
+                                      "on the launch stream around run_iteration (lag mode: the main pass; the "
+                                      "side stream's step-function DP runs beside it and is in the wall time)"},
             "cpu_baseline": (headline_cpu_baseline(committed_cpu_baseline(cpu_workload_key(n_total, Hh, dt, args.month,
                                                                                             args.rl_price if rl else None)), cpu)
                              if (rank == 0 and world == 1) else None),

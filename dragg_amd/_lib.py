@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # DRAGG_LIB: an alternative build of the same library (kernel experiments); default in-tree
 LIB_PATH = os.environ.get("DRAGG_LIB") or os.path.join(HERE, "libdragg_mi355x.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # enums (mirror include/dragg_mi355x.h)
 BASE, PV_ONLY, BATTERY_ONLY, PV_BATTERY = 0, 1, 2, 3
@@ -80,6 +80,15 @@ class Explicit(ctypes.Structure):
                 ("draw", c_dp), ("oat", c_dp), ("ghi", c_dp), ("price", c_dp)]
 
 
+class Lag(ctypes.Structure):
+    _fields_ = [("clock", c_dp), ("skipped", c_dp), ("narrow", c_dp), ("side_workspace", c_dp)]
+
+
+def lag_list_ints(n):
+    """DRAGG_LAG_LIST_INTS(n): a lag-mode list (entries, length, take counter)."""
+    return n + 4
+
+
 NLAUNCH = 4                    # DRAGG_NLAUNCH: hot, big, mid, narrow (dragg_mpc_kernel_info)
 LAUNCH_NAMES = ["hot", "big", "mid", "narrow"]
 
@@ -91,7 +100,8 @@ class KernelInfo(ctypes.Structure):
 
 EXPORTS = ["dragg_mpc_abi_version", "dragg_mpc_strerror", "dragg_mpc_lds_bytes", "dragg_mpc_workspace_bytes",
            "dragg_mpc_kernel_info_get", "dragg_mpc_step",
-           "dragg_mpc_solve_explicit", "dragg_mpc_aggregate", "dragg_mpc_season_noise", "dragg_mpc_reload_knobs"]
+           "dragg_mpc_solve_explicit", "dragg_mpc_aggregate", "dragg_mpc_season_noise", "dragg_mpc_reload_knobs",
+           "dragg_mpc_lag_reset", "dragg_mpc_step_main", "dragg_mpc_step_side", "dragg_mpc_aggregate_rows"]
 
 _LIB = None
 
@@ -126,6 +136,11 @@ def load(path=LIB_PATH):
     lib.dragg_mpc_aggregate.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Hash), c_dp, c_dp]
     lib.dragg_mpc_season_noise.argtypes = [ctypes.POINTER(Dims), ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
                                            ctypes.c_int32, c_dp, c_dp]
+    lib.dragg_mpc_lag_reset.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Lag), ctypes.c_int32, c_dp]
+    for f in (lib.dragg_mpc_step_main, lib.dragg_mpc_step_side):
+        f.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Problem), ctypes.POINTER(Hash), ctypes.POINTER(Out),
+                      ctypes.c_int32, ctypes.POINTER(Lag), c_dp]
+    lib.dragg_mpc_aggregate_rows.argtypes = [ctypes.POINTER(Dims), c_dp, ctypes.c_int32, c_dp, c_dp]
     if lib.dragg_mpc_abi_version() != ABI_VERSION:
         raise DraggError("ABI version mismatch between dragg_amd and libdragg_mi355x.so")
     _LIB = lib

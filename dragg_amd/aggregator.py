@@ -37,7 +37,7 @@ def shard_index(n, rank, world):
 class DeviceAggregator:
     def __init__(self, homes, oat, ghi, tou, start_index=0, num_timesteps=96, reward_price=(0.0,),
                  int_mode="round", seed=0, rank=0, world=1, group=None, keep_history=True,
-                 max_iter=4000, check_every=10, device=None, batch_cls=MPCBatch, exact=False):
+                 max_iter=4000, check_every=10, device=None, batch_cls=MPCBatch, exact=False, overlap=False):
         self.rank, self.world, self.group = rank, world, group
         self.seed = int(seed)
         # identifies the community a checkpoint belongs to (load_state refuses another one's)
@@ -59,16 +59,41 @@ class DeviceAggregator:
         self.hist = (torch.full((num_timesteps, L.NVAL, n), float("nan"), dtype=torch.float64, device=dev)
                      if keep_history else None)
         self.agg_hist = torch.zeros((num_timesteps, 3), dtype=torch.float64, device=dev)
-        self.status_hist = torch.zeros((num_timesteps, n), dtype=torch.int8, device=dev)
+        self.status_hist = torch.zeros((num_timesteps, n), dtype=torch.int32, device=dev)
         self._deferred = []          # steps whose agg_hist row holds this rank's sums only
+        # overlap (lag mode, MPCBatch.enable_lag): a home whose chain needs the slow step-function DP
+        # finishes that step on a side stream while the others go on (run_rbo_mpc has no feedback
+        # between homes, aggregator.py:757-778); its results land in the step's own history rows later,
+        # so the deferred sums are taken from those rows once the side stream has drained.  Needs the
+        # history and keyed season noise; int_mode round.
+        self.overlap = (bool(overlap) and self.hist is not None and int_mode in ("round", "fail") and n > 0
+                        and hasattr(self.batch, "enable_lag"))
+        if self.overlap:
+            self.batch.enable_lag()
+        self._unsummed = []          # lag-mode steps whose agg_hist row is not computed yet
 
     # aggregator.py:711-726
     def run_iteration(self, noise=None):
         t = self.timestep
         hist = self.hist[t] if self.hist is not None else None
-        self.batch.step(t, noise=noise, hist=hist)
-        self.status_hist[t].copy_(self.batch.status, non_blocking=True)
+        if self.overlap and noise is None:
+            self.batch.step_lagged(t, hist, self.status_hist[t])
+        else:
+            self.batch.step(t, noise=noise, hist=hist)
+            self.status_hist[t].copy_(self.batch.status, non_blocking=True)
         self.timestep += 1
+
+    def drain(self):
+        """Overlap mode: wait (in stream order) for the side stream, then fill the sums of the steps
+        that were deferred from their history rows.  Everything a step wrote is readable after this."""
+        d = getattr(self.batch, "drain", None)     # (stand-in batches of the CPU tests have none)
+        if d is not None:
+            d()
+        if self._unsummed:
+            lo, hi = self._unsummed[0], self._unsummed[-1] + 1
+            assert self._unsummed == list(range(lo, hi))
+            self.agg_hist[lo:hi].copy_(self.batch.aggregate_rows(self.hist[lo:hi]))
+            self._unsummed = []
 
     # aggregator.py:728-755 (sums only; the per-home series stay in self.hist)
     def collect_data(self, defer=False):
@@ -77,6 +102,13 @@ class DeviceAggregator:
         so this rank keeps its own sums and reduce_history() all-reduces every deferred step in
         one collective; the ranks then need not meet at every step."""
         t = self.timestep - 1
+        if self.overlap and defer and self.batch.lag["next"] == self.timestep:
+            # (lag mode: the lagging homes' fields of step t are not written yet; drain() sums the row)
+            self._unsummed.append(t)
+            if self.world > 1:
+                self._deferred.append(t)
+            return None
+        self.drain()
         agg = self.batch.aggregate()
         if self.world > 1:
             if defer:
@@ -88,6 +120,7 @@ class DeviceAggregator:
 
     def reduce_history(self):
         """All-reduce the deferred steps' sums (one RCCL call); agg_hist is then community-wide."""
+        self.drain()
         if self._deferred:
             idx = torch.tensor(self._deferred, dtype=torch.long, device=self.agg_hist.device)
             rows = self.agg_hist.index_select(0, idx)
@@ -120,9 +153,11 @@ class DeviceAggregator:
         return t
 
     def snapshot(self):
+        self.drain()
         return self.timestep, self.batch.vals.clone(), self.batch.fc.clone()
 
     def restore(self, snap):
+        self.drain()
         t, vals, fc = snap
         self.timestep = t
         self.batch.vals.copy_(vals)
@@ -152,6 +187,7 @@ class DeviceAggregator:
     # price -- plus the histories, one file per rank.  The season-noise stream is keyed by
     # (seed, home, t), so a resumed run continues bit for bit as if it had not stopped.
     def save_state(self, path):
+        self.drain()
         t = self.timestep
         state = {"timestep": t, "rank": self.rank, "world": self.world, "n_local": int(self.batch.N),
                  "seed": self.seed, "num_timesteps": int(self.num_timesteps), "n_all": len(self.all_homes),
@@ -168,6 +204,7 @@ class DeviceAggregator:
 
     def load_state(self, path):
         """Resume from save_state's file (tensors only: loaded with weights_only=True)."""
+        self.drain()
         st = torch.load(path, map_location="cpu", weights_only=True)
         if (st["rank"], st["world"], st["n_local"]) != (self.rank, self.world, int(self.batch.N)):
             raise ValueError(f"checkpoint {path} is for rank {st['rank']} of {st['world']} with "
@@ -229,6 +266,7 @@ class DeviceAggregator:
         """Raise as the reference would if a home hit a crashing path (KeyError / ValueError):
         the first such (timestep, home) over EVERY rank, raised on every rank together (one
         all-reduce), so a multi-rank run stops instead of leaving the other ranks in a gather."""
+        self.drain()
         st = self.status_hist[:self.timestep].cpu().numpy()
         n_all = max(1, len(self.all_homes))
         first = np.iinfo(np.int64).max
@@ -253,10 +291,12 @@ class DeviceAggregator:
         """This shard's `collected_data` dict (aggregator.py:589-615, 737-748): the initial
         entries plus every step's hash fields, in the reference's key order."""
         from . import results as R
+        self.drain()
         hist = self.hist[:self.timestep].cpu().numpy()
         return R.append_history(R.new_collected(self.homes), self.homes, hist)
 
     def summary(self):
+        self.drain()
         agg = self.agg_hist[:self.timestep].cpu().numpy()
         return {"p_grid_aggregate": agg[:, 0].tolist(), "forecast_load": agg[:, 1].tolist(),
                 "agg_cost": agg[:, 2].tolist(), "p_max_aggregate": float(agg[:, 0].max()) if len(agg) else None}

@@ -1203,7 +1203,31 @@ struct KArgs {
     const double* noise;
     int t;
     int force_steps;       // diagnostic (DRAGG_FORCE_STEP_DP=1): every home to the exact step DP
+    // lag mode (dragg_mpc_step_main / _side): homes whose previous step is still being solved on the
+    // side stream are skipped by the main pass and solved by the side pass after it
+    char* lws;             // the lists and per-block scratch regions (NULL: problem.workspace's)
+    int* clk;              // [N] timesteps completed per home (LAG_SIDE set: completed by the side pass)
+    int* skip;             // step_main: homes whose clock is behind, for the side pass (list)
+    int* hot_list;         // step_side: the hot launch takes its homes off this list
+    int* nar;              // the step-function DP's list (NULL: the workspace's)
+    int side;              // 1 in the side pass: its completions publish with a release
 };
+
+// a clock value the side pass wrote: the reader must acquire before it reads the home's rows
+constexpr int LAG_SIDE = 1 << 30;
+
+// lag mode: the home's step is complete (every thread of the block calls it, after every write of the
+// home): its clock moves to t + 1.  The main pass's next step reads it in stream order; a side-pass
+// completion is read by a CONCURRENT main-pass kernel, so its writes are released first (agent scope:
+// the other XCDs' L2s) and the clock carries LAG_SIDE so that the reader acquires
+DEV void lag_finish(const KArgs& a, int home) {
+    if (!a.clk) return;
+    if (a.side) __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(a.clk + home, (a.t + 1) | (a.side ? LAG_SIDE : 0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // --------------------------------------------------------------------------------------
 // kernel prologue shared by both solve paths: per-home constants, the step's inputs
@@ -3793,10 +3817,11 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
     const int lane = threadIdx.x;
     const int N = a.d.n_homes;
     const int H = a.d.horizon;
-    char* const ws = reinterpret_cast<char*>(a.p.workspace);
-    int* const list = reinterpret_cast<int*>(ws + defer_offset(N, H));     // [N] + length at [N]
-    int* const nlist = reinterpret_cast<int*>(ws + narrow_list_offset(N, H));   // DM_MID / DM_BUCKET -> DM_NARROW
-    int* const blist = reinterpret_cast<int*>(ws + mid_list_offset(N, H));      // DM_MID -> DM_BUCKET
+    char* const ws = reinterpret_cast<char*>(a.p.workspace);            // per-home rows
+    char* const lw = a.lws ? a.lws : ws;                                 // lists, per-block scratch
+    int* const list = reinterpret_cast<int*>(lw + defer_offset(N, H));     // [N] + length at [N]
+    int* const nlist = a.nar ? a.nar : reinterpret_cast<int*>(lw + narrow_list_offset(N, H));   // -> DM_NARROW
+    int* const blist = reinterpret_cast<int*>(lw + mid_list_offset(N, H));      // DM_MID -> DM_BUCKET
     Home h;
     LdsD D = MODE == DM_FRONT ? carve_front(smem, H) : carve_direct(smem, H, a.d.sub_steps);
     D.par = reinterpret_cast<uint16_t*>(ws) + (size_t)home * H * NB_CAP;
@@ -3811,6 +3836,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
         if (lane == 0) {
             write_missing(a, home);
         }
+        lag_finish(a, home);
         return;
     }
     derive(h);
@@ -3895,7 +3921,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 // the exact step-function DP (any prices, any feasible sets)
                 const NarrowLayout nl = narrow_layout(H, a.d.sub_steps);
                 char* const sb = reinterpret_cast<char*>(smem);
-                double* const sw = reinterpret_cast<double*>(ws + narrow_region_offset(N, H) +
+                double* const sw = reinterpret_cast<double*>(lw + narrow_region_offset(N, H) +
                                                              (size_t)slot * step_slot_bytes());
                 int* const swi = reinterpret_cast<int*>(sw + 2 * (size_t)POOL_CAP);
                 double2* const swr = reinterpret_cast<double2*>(swi + 2 * (size_t)MC_CAP);
@@ -4053,8 +4079,8 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                     char* const sb = reinterpret_cast<char*>(smem);
                     double* const wl = reinterpret_cast<double*>(sb + bl.wl);
                     uint16_t* const bpar = MODE == DM_MID
-                        ? reinterpret_cast<uint16_t*>(ws + mid_region_offset(N, H)) + (size_t)slot * H * NF_MID
-                        : reinterpret_cast<uint16_t*>(ws + big_region_offset(N, H)) + (size_t)slot * H * NF_BIG;
+                        ? reinterpret_cast<uint16_t*>(lw + mid_region_offset(N, H)) + (size_t)slot * H * NF_MID
+                        : reinterpret_cast<uint16_t*>(lw + big_region_offset(N, H)) + (size_t)slot * H * NF_BIG;
                     const FrontBufs FB{reinterpret_cast<double2*>(sb + bl.fa), reinterpret_cast<double2*>(sb + bl.fb),
                                        reinterpret_cast<unsigned long long*>(sb + bl.kb),
                                        reinterpret_cast<unsigned long long*>(sb + bl.cb),
@@ -4132,15 +4158,30 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
     pf.mark(DRAGG_PH_WRITE);
     if (pf.on && lane == 0)
         for (int k = 0; k < DRAGG_NPHASE; ++k) a.out.cycles[(size_t)k * N + home] = (int64_t)pf.acc[k];
+    lag_finish(a, home);
 }
 
 template <bool EXPLICIT, int MODE, int NW = 1>
 __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW ? 1 : 2) void mpc_direct_kernel(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    char* const ws = reinterpret_cast<char*>(a.p.workspace);
+    char* const ws = a.lws ? a.lws : reinterpret_cast<char*>(a.p.workspace);
     const int N = a.d.n_homes, H = a.d.horizon;
-    if (MODE == DM_FRONT) {
-        if ((int)blockIdx.x < N) solve_direct<EXPLICIT, MODE, NW>(a, blockIdx.x, smem, 0, 0);
+    __shared__ int take;
+    if (MODE == DM_FRONT && !a.hot_list) {
+        const int home = blockIdx.x;
+        if (home >= N) return;
+        if (a.clk) {
+            // lag mode, main pass: a home whose previous step is not complete yet goes to the side pass
+            if (threadIdx.x == 0) take = __hip_atomic_load(a.clk + home, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            const int c = take;
+            if ((c & ~LAG_SIDE) != a.t) {
+                if (threadIdx.x == 0) a.skip[atomicAdd(a.skip + N, 1)] = home;
+                return;
+            }
+            if (c & LAG_SIDE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the side pass's rows
+        }
+        solve_direct<EXPLICIT, MODE, NW>(a, home, smem, 0, 0);
         return;
     }
     // persistent: block b solves listed home b first, then takes the next ones off a shared counter
@@ -4149,9 +4190,10 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
     // b); blocks past the list's length leave at once, every block reaches its end and exits
     const size_t lo = MODE == DM_MID ? defer_offset(N, H) : MODE == DM_BUCKET ? mid_list_offset(N, H)
                     : narrow_list_offset(N, H);
-    int* const list = reinterpret_cast<int*>(ws + lo);
+    // (the side pass's hot launch: the skipped homes; both passes' DM_NARROW in lag mode: the step's list)
+    int* const list = MODE == DM_FRONT ? a.hot_list : (MODE == DM_NARROW && a.nar) ? a.nar
+                    : reinterpret_cast<int*>(ws + lo);
     const int cnt = min(list[N], N);
-    __shared__ int take;
     for (int j = blockIdx.x; j < cnt;) {
         const int e = list[j];                      // home | flags | deferred chain << 30
         const int home = e & HOME_MASK, chain = (e >> 30) & 1;
@@ -4163,19 +4205,24 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
     }
 }
 
-// the three device lists' (length, take counter) pairs to zero before a step's launches
-__global__ void reset_lists_kernel(int* a, int* b, int* c) {
+// the device lists' (length, take counter) pairs to zero before a step's launches (NULL: none)
+__global__ void reset_lists_kernel(int* a, int* b, int* c, int* d, int* e) {
     const int i = threadIdx.x;
-    if (i < 2) a[i] = 0;
-    else if (i < 4) b[i - 2] = 0;
-    else if (i < 6) c[i - 4] = 0;
+    int* const p = i < 2 ? a : i < 4 ? b : i < 6 ? c : i < 8 ? d : i < 10 ? e : nullptr;
+    if (p) p[i & 1] = 0;
+}
+
+// lag mode: every home's clock = t (the state the host holds: every step before t complete)
+__global__ void lag_reset_kernel(int* clk, int N, int t) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) clk[i] = t;
 }
 
 // collect_data's three sums (aggregator.py:728-755) in one 1024-thread block: 16 waves of
 // independent loads (a step's sums are a latency-bound 240 KB read at 10k homes), then a wave
 // reduction and a pass over the 16 wave partials
 constexpr int AGG_NT = 1024;
-__global__ __launch_bounds__(AGG_NT) void aggregate_kernel(const double* vals, int N, double* out3) {
+DEV void agg_sums(const double* vals, int N, double* out3) {
     __shared__ double red[3][AGG_NT / WAVE];
     const double* p0 = vals + (size_t)DRAGG_K_P_GRID * N;
     const double* p1 = vals + (size_t)DRAGG_K_FORECAST_P_GRID * N;
@@ -4195,6 +4242,14 @@ __global__ __launch_bounds__(AGG_NT) void aggregate_kernel(const double* vals, i
         for (int i = 0; i < AGG_NT / WAVE; ++i) t += red[threadIdx.x][i];
         out3[threadIdx.x] = t;
     }
+}
+__global__ __launch_bounds__(AGG_NT) void aggregate_kernel(const double* vals, int N, double* out3) {
+    agg_sums(vals, N, out3);
+}
+// the sums of many steps at once, from the history rows the steps wrote ([rows][NVAL][N]): block r
+// sums row r exactly as aggregate_kernel sums vals (the same code: bit-identical)
+__global__ __launch_bounds__(AGG_NT) void aggregate_rows_kernel(const double* rows, int N, double* out) {
+    agg_sums(rows + (size_t)blockIdx.x * DRAGG_NVAL * N, N, out + (size_t)blockIdx.x * 3);
 }
 
 __global__ void noise_kernel(int N, int H, uint64_t seed, int off, int stride, int t, double* out) {
@@ -4325,7 +4380,7 @@ int launch(const KArgs& a, hipStream_t s) {
     b.force_steps = knobs().force_steps;
     // each list's length and the persistent launch's take counter after it, in one tiny launch
     // (three 8-byte memsets cost three fills: ~13 us of a 0.49 ms step at 1,250 homes)
-    hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, nlen, blen);
+    hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, nlen, blen, nullptr, nullptr);
     if (hipGetLastError() != hipSuccess) return DRAGG_E_HIP;
     const size_t lds = kernel_lds_bytes(&a.d);
     const int nw = hot_waves();
@@ -4346,6 +4401,62 @@ int launch(const KArgs& a, hipStream_t s) {
     const int rcn = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_NARROW, NT_STEPS / WAVE>, attr[5], b, min(N, NARROW_SLOTS),
                                   NT_STEPS, (size_t)narrow_layout(a.d.horizon, a.d.sub_steps).bytes, s);
     return rcn;
+}
+
+// Lag mode: one timestep in two passes on two streams (the caller orders them: the side pass of step t
+// after the main pass of step t, the main pass of step t + R after the side pass of step t when the
+// caller's list ring holds R steps).
+//  main: the hot launch over every home whose clock is at t (the others -- their previous step still on
+//        the side stream -- listed in lag->skipped), the mid and big launches; the chains left for the
+//        step-function DP go to lag->narrow and are NOT solved here;
+//  side: the skipped homes' whole step (hot launch over lag->skipped, mid, big -- its own lists and
+//        per-block scratch in lag->side_workspace) and the step-function DP over lag->narrow.
+// A home's clock moves to t + 1 when its step is complete; so the next main pass solves every home
+// whose step-function DP finished in time and leaves the others to the side stream, which runs behind.
+constexpr int SIDE_HOT_BLOCKS = 256;        // persistent blocks of the side pass's hot launch
+constexpr int SIDE_NARROW_BLOCKS = 8;       // ... of its step-function launch (each needs a whole CU's LDS)
+int launch_lag(const KArgs& a, bool side, hipStream_t s) {
+    static int attr_dev[MAX_DEV][8] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return DRAGG_E_HIP;
+    int* const attr = attr_dev[dev];
+    const int N = a.d.n_homes, H = a.d.horizon;
+    if (N == 0) return DRAGG_OK;
+    char* const lw = a.lws;
+    int* const len = reinterpret_cast<int*>(lw + defer_offset(N, H)) + N;
+    int* const blen = reinterpret_cast<int*>(lw + mid_list_offset(N, H)) + N;
+    KArgs b = a;
+    b.force_steps = 0;
+    const size_t lds = kernel_lds_bytes(&a.d);
+    if (!side) {
+        hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, blen, a.skip + N, a.nar + N, nullptr);
+        if (hipGetLastError() != hipSuccess) return DRAGG_E_HIP;
+        b.hot_list = nullptr;
+        b.side = 0;
+        int rc = launch_kernel(mpc_direct_kernel<false, DM_FRONT, 1>, attr[1], b, N, WAVE, lds, s);
+        if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_MID, NW_MID>, attr[6], b,
+                                    min(N, mid_slots<false>(dev, H, a.d.sub_steps)), NW_MID * WAVE,
+                                    (size_t)mid_layout(H, a.d.sub_steps).bytes, s);
+        if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_BUCKET, NW_BIG>, attr[2], b, min(N, SECOND_SLOTS),
+                                    NW_BIG * WAVE, (size_t)big_layout(H, a.d.sub_steps).bytes, s);
+        return rc;
+    }
+    // (lag->skipped and lag->narrow were zeroed by the main pass, which filled them)
+    hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, blen, nullptr, nullptr, nullptr);
+    if (hipGetLastError() != hipSuccess) return DRAGG_E_HIP;
+    b.hot_list = a.skip;
+    b.skip = nullptr;
+    b.side = 1;
+    int rc = launch_kernel(mpc_direct_kernel<false, DM_FRONT, 1>, attr[0], b, min(N, SIDE_HOT_BLOCKS), WAVE, lds, s);
+    b.hot_list = nullptr;
+    if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_MID, NW_MID>, attr[6], b,
+                                min(N, mid_slots<false>(dev, H, a.d.sub_steps)), NW_MID * WAVE,
+                                (size_t)mid_layout(H, a.d.sub_steps).bytes, s);
+    if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_BUCKET, NW_BIG>, attr[2], b, min(N, SECOND_SLOTS),
+                                NW_BIG * WAVE, (size_t)big_layout(H, a.d.sub_steps).bytes, s);
+    if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_NARROW, NT_STEPS / WAVE>, attr[5], b,
+                                min(N, SIDE_NARROW_BLOCKS), NT_STEPS, (size_t)narrow_layout(H, a.d.sub_steps).bytes, s);
+    return rc;
 }
 
 }  // namespace
@@ -4394,6 +4505,62 @@ int dragg_mpc_step(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob, dr
     a.d = *dims; a.p = *prob; a.vals = hash->vals; a.fc = hash->fc; a.out = *out; a.noise = noise;
     a.t = timestep;
     return launch<false>(a, (hipStream_t)stream);
+}
+
+static int lag_args(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob, dragg_mpc_hash* hash,
+                    dragg_mpc_out* out, int32_t timestep, const dragg_mpc_lag* lag, bool side, KArgs* a) {
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    if (!direct_mode(dims) || !lag || !prob || !hash || !out || timestep < 0) return DRAGG_E_ARG;
+    if (dims->n_homes == 0) return DRAGG_OK;
+    if (!lag->clock || !lag->skipped || !lag->narrow || (side && !lag->side_workspace) || !prob->params ||
+        !prob->home_type || !prob->oat || !prob->ghi || !prob->tou || !prob->reward_price || !prob->draw_hourly ||
+        !prob->workspace || !hash->vals || !hash->fc || !out->status || !out->iters || !out->obj || !out->relax_obj)
+        return DRAGG_E_ARG;
+    if (dims->n_rp != 1 && dims->n_rp < dims->horizon) return DRAGG_E_ARG;
+    if (prob->start_index + timestep + dims->horizon >= dims->n_env) return DRAGG_E_ARG;
+    if (timestep >= LAG_SIDE - 1) return DRAGG_E_ARG;
+    *a = KArgs{};
+    a->d = *dims; a->p = *prob; a->vals = hash->vals; a->fc = hash->fc; a->out = *out; a->noise = nullptr;
+    a->t = timestep;
+    a->lws = reinterpret_cast<char*>(side ? lag->side_workspace : prob->workspace);
+    a->clk = lag->clock; a->skip = lag->skipped; a->nar = lag->narrow;
+    return DRAGG_OK;
+}
+
+int dragg_mpc_step_main(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob, dragg_mpc_hash* hash,
+                        dragg_mpc_out* out, int32_t timestep, const dragg_mpc_lag* lag, void* stream) {
+    KArgs a;
+    const int rc = lag_args(dims, prob, hash, out, timestep, lag, false, &a);
+    if (rc || dims->n_homes == 0) return rc;
+    return launch_lag(a, false, (hipStream_t)stream);
+}
+
+int dragg_mpc_step_side(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob, dragg_mpc_hash* hash,
+                        dragg_mpc_out* out, int32_t timestep, const dragg_mpc_lag* lag, void* stream) {
+    KArgs a;
+    const int rc = lag_args(dims, prob, hash, out, timestep, lag, true, &a);
+    if (rc || dims->n_homes == 0) return rc;
+    return launch_lag(a, true, (hipStream_t)stream);
+}
+
+int dragg_mpc_lag_reset(const dragg_mpc_dims* dims, const dragg_mpc_lag* lag, int32_t timestep, void* stream) {
+    if (!dims || dims->n_homes < 0 || !lag || timestep < 0 || timestep >= LAG_SIDE - 1) return DRAGG_E_ARG;
+    if (dims->n_homes == 0) return DRAGG_OK;
+    if (!lag->clock) return DRAGG_E_ARG;
+    hipLaunchKernelGGL(lag_reset_kernel, dim3((dims->n_homes + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       lag->clock, dims->n_homes, timestep);
+    return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
+}
+
+int dragg_mpc_aggregate_rows(const dragg_mpc_dims* dims, const double* rows, int32_t n_rows, double* out,
+                             void* stream) {
+    if (!dims || dims->n_homes < 0 || n_rows < 0 || (n_rows > 0 && (!out || (!rows && dims->n_homes > 0))))
+        return DRAGG_E_ARG;
+    if (n_rows == 0) return DRAGG_OK;
+    hipLaunchKernelGGL(aggregate_rows_kernel, dim3(n_rows), dim3(AGG_NT), 0, (hipStream_t)stream, rows,
+                       dims->n_homes, out);
+    return hipGetLastError() == hipSuccess ? DRAGG_OK : DRAGG_E_HIP;
 }
 
 int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob,

@@ -158,6 +158,7 @@ class MPCBatch:
         if ws < 0:
             L.check(int(ws))
         self.workspace = torch.empty(max(1, (ws + 7) // 8), dtype=torch.int64, device=dev) if ws > 0 else None
+        self.lag = None
 
     # ------------------------------------------------------------------ environment
     def set_environment(self, oat, ghi, tou, start_index):
@@ -208,7 +209,95 @@ class MPCBatch:
     def step(self, t, noise=None, hist=None, stream=None):
         """One closed-loop timestep for every home (run_iteration, aggregator.py:711-726)."""
         with torch.cuda.device(self.device):
+            self.drain(stream)
+            if self.lag is not None:
+                self.lag["next"] = None          # the clocks no longer describe the state
             return self._step(t, noise, hist, stream)
+
+    # ------------------------------------------------------------------ lag mode
+    def enable_lag(self, ring=128):
+        """Lag mode (dragg_mpc_step_main / _side, include/dragg_mi355x.h): a home whose chain needs the
+        step-function DP finishes that step on a side stream while the other homes go on with their
+        next steps; it catches up there.  Allocates the side pass's workspace, the per-home clocks, a
+        ring of `ring` per-step list pairs (the main pass of step t + ring waits for the side pass of
+        step t), the side stream and the events that order the two passes."""
+        if self.dims.int_mode not in (L.INT_ROUND, L.INT_FAIL):
+            raise ValueError("lag mode needs int_mode 'round' (or 'fail')")
+        dev = self.device
+        with torch.cuda.device(dev):
+            self.lag = {
+                "ring": int(ring),
+                "lists": torch.zeros((ring, 2, L.lag_list_ints(self.N)), dtype=torch.int32, device=dev),
+                "clock": torch.zeros(max(1, self.N), dtype=torch.int32, device=dev),
+                "side_ws": torch.empty_like(self.workspace) if self.workspace is not None else None,
+                "stream": torch.cuda.Stream(device=dev),
+                "main_done": torch.cuda.Event(),
+                "side_done": [torch.cuda.Event() for _ in range(ring)],
+                "recorded": [False] * ring,
+                "next": None,                   # the step the clocks are ready for
+                "pending": False,               # side work not yet joined into the main stream
+            }
+
+    def step_lagged(self, t, hist, status_row, stream=None):
+        """One timestep in lag mode: the main pass on `stream` (default: the current one), the side pass
+        on the side stream after it.  `hist` ([NVAL][N]) and `status_row` ([N] int32) receive the step's
+        per-home results -- a lagging home's later -- so they must be this step's own rows; nothing of
+        the step may be read before drain()."""
+        with torch.cuda.device(self.device):
+            return self._step_lagged(t, hist, status_row, stream)
+
+    def _step_lagged(self, t, hist, status_row, stream):
+        lg = self.lag
+        if lg is None:
+            raise RuntimeError("enable_lag() first")
+        assert hist is not None and status_row is not None and status_row.dtype == torch.int32
+        main = stream if stream is not None else torch.cuda.current_stream(self.device)
+        side = lg["stream"]
+        slot = t % lg["ring"]
+        lag = L.Lag(clock=L.ptr(lg["clock"]), skipped=L.ptr(lg["lists"][slot, 0]), narrow=L.ptr(lg["lists"][slot, 1]),
+                    side_workspace=L.ptr(lg["side_ws"]))
+        if lg["next"] != t:
+            # (the first lag-mode step, or one after a serial step: every step before t is complete)
+            self.drain(main)
+            L.check(self.lib.dragg_mpc_lag_reset(ctypes.byref(self.dims), ctypes.byref(lag), int(t),
+                                                  L.stream_ptr(main, self.device)))
+        if lg["recorded"][slot]:
+            main.wait_event(lg["side_done"][slot])      # the side pass of step t - ring is done with the lists
+        prob, hsh = self._problem(), self._hash()
+        out = L.Out(status=L.ptr(status_row), iters=L.ptr(self.iters), obj=L.ptr(self.obj),
+                    relax_obj=L.ptr(self.relax_obj), hist=L.ptr(hist), cycles=None, int_path=L.ptr(self.int_path))
+        L.check(self.lib.dragg_mpc_step_main(ctypes.byref(self.dims), ctypes.byref(prob), ctypes.byref(hsh),
+                                             ctypes.byref(out), int(t), ctypes.byref(lag), L.stream_ptr(main, self.device)))
+        lg["main_done"].record(main)
+        side.wait_event(lg["main_done"])
+        L.check(self.lib.dragg_mpc_step_side(ctypes.byref(self.dims), ctypes.byref(prob), ctypes.byref(hsh),
+                                             ctypes.byref(out), int(t), ctypes.byref(lag), L.stream_ptr(side, self.device)))
+        lg["side_done"][slot].record(side)
+        lg["recorded"][slot] = True
+        lg["last"] = slot
+        lg["next"] = t + 1
+        lg["pending"] = True
+        self._keep = (hist, status_row)
+
+    def drain(self, stream=None):
+        """Join the side stream into `stream` (default: the current one): after this, everything the
+        lag-mode steps wrote is visible in stream order."""
+        lg = self.lag
+        if lg is None or not lg["pending"]:
+            return
+        main = stream if stream is not None else torch.cuda.current_stream(self.device)
+        main.wait_event(lg["side_done"][lg["last"]])
+        lg["pending"] = False
+
+    def aggregate_rows(self, rows, stream=None):
+        """collect_data sums of every history row of `rows` ([T][NVAL][N]) -> [T][3] (bit-identical to
+        aggregate() on each row)."""
+        with torch.cuda.device(self.device):
+            out = torch.empty((rows.shape[0], 3), dtype=torch.float64, device=self.device)
+            L.check(self.lib.dragg_mpc_aggregate_rows(ctypes.byref(self.dims), L.ptr(rows.contiguous()),
+                                                      int(rows.shape[0]), L.ptr(out),
+                                                      L.stream_ptr(stream, self.device)))
+            return out
 
     def _step(self, t, noise, hist, stream):
         if noise is not None:
@@ -226,6 +315,7 @@ class MPCBatch:
             return self._solve_explicit(t, T0, Tw0, E0, counter, winter, draw, oat, ghi, price, stream)
 
     def _solve_explicit(self, t, T0, Tw0, E0, counter, winter, draw, oat, ghi, price, stream):
+        self.drain(stream)
         dev, N, H = self.device, self.N, self.H
 
         def d(x, shape, dtype=torch.float64):
@@ -254,6 +344,7 @@ class MPCBatch:
             return self._aggregate(stream)
 
     def _aggregate(self, stream):
+        self.drain(stream)
         hsh = self._hash()
         L.check(self.lib.dragg_mpc_aggregate(ctypes.byref(self.dims), ctypes.byref(hsh), L.ptr(self.agg),
                                              L.stream_ptr(stream, self.device)))
@@ -273,6 +364,7 @@ class MPCBatch:
     # ------------------------------------------------------------------ hash views
     def hash_dict(self, i, as_str=True):
         """The home's redis hash as `hgetall` would return it (str values, absent fields omitted)."""
+        self.drain()
         vals = self.vals[:, i].cpu().numpy()
         fc = self.fc[:, :, i].cpu().numpy()
         out = {}

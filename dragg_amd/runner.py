@@ -102,6 +102,9 @@ class Aggregator:
                                     self.num_timesteps, reward_price=self.reward_price, int_mode=self.int_mode,
                                     seed=int(self.config["simulation"]["random_seed"]), rank=self.rank,
                                     world=self.world, group=self.group, device=self.device,
+                                    # run_rbo_mpc: a home in its step-function DP does not hold up the
+                                    # others (lag mode, DeviceAggregator); results are bit-identical
+                                    overlap=getattr(self, "case", None) == "baseline",
                                     **({"batch_cls": self.batch_cls} if self.batch_cls else {}))
         return self.dev
 
@@ -267,6 +270,7 @@ class Aggregator:
         Incremental: each call brings over only the steps since the previous one (a checkpoint
         then costs its own rows, not the whole run again), as one tensor gather of the shards
         padded to a common width (NCCL on the device, gloo on the host) -- no pickling."""
+        self.dev.drain()
         T = self.dev.timestep
         t0 = getattr(self, "_hist_rows", 0)
         if t0 == 0:

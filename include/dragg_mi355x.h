@@ -18,7 +18,10 @@
  *     cleanup_and_finish      mpc_calc.py:476     (success extraction / fallback thermostat)
  *     redis_write_optimal_vals mpc_calc.py:100    (hash arrays updated in place)
  *   manage_home + ProcessPool aggregator.py:723   one launch over all homes of a timestep
- *   collect_data sums         aggregator.py:751   dragg_mpc_aggregate()
+ *   collect_data sums         aggregator.py:751   dragg_mpc_aggregate() / dragg_mpc_aggregate_rows()
+ *   run_baseline's loop       aggregator.py:757   dragg_mpc_step_main() + dragg_mpc_step_side()
+ *                                                  (lag mode: a home still in its step-function DP
+ *                                                  does not hold up the other homes' next steps)
  *   MPCCalc per-solve (explicit inputs)         dragg_mpc_solve_explicit()
  *
  * Conventions
@@ -42,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DRAGG_MPC_ABI_VERSION 7
+#define DRAGG_MPC_ABI_VERSION 8
 
 /* home types (aggregator.py:425, 468, 520, 555); bit 0 = pv, bit 1 = battery */
 enum dragg_home_type {
@@ -178,9 +181,12 @@ typedef struct dragg_mpc_out {
     int32_t* int_path;          /* optional [N] integer-DP path (int_mode round): 0 = the
                                    exact front DP solved both thermal chains; bit 0 / bit 1
                                    = the indoor-air / tank chain kept an approximate (feasible)
-                                   schedule; bits 4-7 / 8-11 its reason -- since v7 only
-                                   6: the exact step-function DP past its capacity (its pool
-                                   of 2^20 breakpoints per chain; never measured); bit 12 = solved by a later launch (its front
+                                   schedule; bits 4-7 / 8-11 its reason: 3 = an RL-priced chain
+                                   (a price change at more than H/4 stages) whose front passed
+                                   the big launch's 2,048 labels keeps its bucketed schedule
+                                   (default build; DRAGG_FLAG_EXACT sends it to the step-function
+                                   DP), 6 = the exact step-function DP past its capacity (its pool
+                                   of 2^20 breakpoints per chain); bit 12 = solved by a later launch (its front
                                    outgrew the hot launch's capacity; still exact when
                                    bits 0-11 are 0); bits 13 / 14 = status ROUND_FAIL
                                    decided by the indoor-air / tank chain (no integer duty
@@ -269,6 +275,45 @@ int dragg_mpc_kernel_info_get(const dragg_mpc_dims* dims, dragg_mpc_kernel_info*
    the reference would have crashed on, KeyError at aggregator.py:750-752) makes its sum NaN. */
 int dragg_mpc_aggregate(const dragg_mpc_dims* dims, const dragg_mpc_hash* hash, double* out3,
                         void* stream);
+
+/* Lag mode (since v8): run_rbo_mpc's timestep loop (aggregator.py:757-778) has no feedback between
+   homes, so a home whose chain needs the slow exact step-function DP need not hold up the others.
+   A step is split into two passes the caller puts on two streams:
+     dragg_mpc_step_main(t)  on the main stream: every home whose clock is at t (its previous step
+                             complete) is solved by the hot / mid / big launches; a home whose clock
+                             is behind is listed in `skipped`; chains left for the step-function DP
+                             are listed in `narrow` (not solved here);
+     dragg_mpc_step_side(t)  on the side stream, AFTER main(t) (an event): the skipped homes' whole
+                             step (their own lists and per-block scratch in side_workspace) and the
+                             step-function DP of every chain in `narrow`.
+   A home's clock becomes t + 1 when its step is complete (a side-pass completion is published to
+   the concurrently running main pass with an agent-scope release).  Each step needs its own
+   skipped / narrow lists until its side pass has run: with a ring of R list pairs the main pass of
+   step t + R must wait for the side pass of step t.  Results are bit-identical to dragg_mpc_step's
+   (every home's solve is the same code on the same inputs), but per-step outputs of lagging homes
+   land later: the caller reads them (status -- out.status should then be a per-step row --, hist
+   rows, vals/fc) only after the side stream has drained, and takes collect_data's sums from the
+   history rows (dragg_mpc_aggregate_rows).  Keyed season noise only (the NULL-noise stream);
+   int_mode round / fail only. */
+typedef struct dragg_mpc_lag {
+    int32_t* clock;             /* [N] timesteps completed per home (dragg_mpc_lag_reset) */
+    int32_t* skipped;           /* [DRAGG_LAG_LIST_INTS(N)] the step's homes left to the side pass */
+    int32_t* narrow;            /* [DRAGG_LAG_LIST_INTS(N)] the step's step-function DP chains   */
+    void* side_workspace;       /* dragg_mpc_workspace_bytes(dims) bytes, the side pass's own     */
+} dragg_mpc_lag;
+#define DRAGG_LAG_LIST_INTS(n) ((n) + 4)
+
+/* clock[] = timestep for every home (before the first lag-mode step after any other kind of step) */
+int dragg_mpc_lag_reset(const dragg_mpc_dims* dims, const dragg_mpc_lag* lag, int32_t timestep, void* stream);
+int dragg_mpc_step_main(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob, dragg_mpc_hash* hash,
+                        dragg_mpc_out* out, int32_t timestep, const dragg_mpc_lag* lag, void* stream);
+int dragg_mpc_step_side(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob, dragg_mpc_hash* hash,
+                        dragg_mpc_out* out, int32_t timestep, const dragg_mpc_lag* lag, void* stream);
+
+/* collect_data's sums of n_rows steps from their history rows ([n_rows][DRAGG_NVAL][N], the
+   dragg_mpc_out.hist copies): out[r][3] exactly as dragg_mpc_aggregate on row r (bit-identical). */
+int dragg_mpc_aggregate_rows(const dragg_mpc_dims* dims, const double* rows, int32_t n_rows, double* out,
+                             void* stream);
 
 /* The keyed season-noise stream used when noise == NULL: writes [H][N] normals for
    timestep t (exposed so the host and tests can reproduce the draw); home i of the shard
