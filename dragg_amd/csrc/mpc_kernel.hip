@@ -49,6 +49,9 @@ constexpr int NARROW_SLOTS = 16;         // blocks of the persistent DM_NARROW l
 // the exact step-function DP (dp_steps, DM_NARROW)
 constexpr int NP_CAP = 32768;             // breakpoints of one V_k
 constexpr int POOL_CAP = 1 << 20;         // breakpoints of all V_k of one chain (the pool)
+// merge points over the stages of one step-function DP pass: a bound on one chain's work (~40 ms at the
+// measured ~25 M merge points/s of one block); the bench's narrow chains take 74-160 k
+constexpr long long STEP_WORK_CAP = 2000000;
 constexpr int STEP_MAXU = 16;             // duty values 0..S (S <= 15)
 constexpr int MC_CAP = 8 * NP_CAP;        // merged candidate points of one stage ((S + 1) np, S <= 7)
 constexpr int STEP_CH = 8;                // merged outputs per merge work item, at most (fewer on small stages)
@@ -1211,6 +1214,8 @@ struct KArgs {
     int* hot_list;         // step_side: the hot launch takes its homes off this list
     int* nar;              // the step-function DP's list (NULL: the workspace's)
     int side;              // 1 in the side pass: its completions publish with a release
+    int step_pool_cap;     // the step-function DP's pool per chain (POOL_CAP; a diagnostic knob shrinks it)
+    long long step_work_cap;   // ... its work bound per pass (0: STEP_WORK_CAP)
 };
 
 // a clock value the side pass wrote: the reader must acquire before it reads the home's rows
@@ -3223,6 +3228,8 @@ struct StepBufs {
                                   //   minimiser and minimum (the cost pruning)
     char* sp;                     // LDS pool [spb] bytes: per stage V_{k+1} (B, V) and the merge buffers
     int spb;                      //   (lp_cut: the waves' PL tables)
+    int pool_cap;                 // breakpoints of all V_k of the chain (<= POOL_CAP; a knob shrinks it)
+    long long work_cap;           // merge points over all stages of one pass: the work bound of a chain
 };
 
 // exclusive prefix sums over the NT threads of the block of v[0..n) (n <= STEP_MAXU), in place
@@ -3448,6 +3455,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         if (tid == 0) { Sb.PB[0] = l; Sb.PB[1] = u; Sb.PV[0] = 0.0; Sb.off[H] = 0; Sb.cnt[H] = 1; }
     }
     int top = 2;                                          // next free pool entry (every thread)
+    long long work = 0;                                   // merge points so far (the work bound)
     __syncthreads();
 #ifdef DRAGG_STEP_PROF
     unsigned long long sp_t = __builtin_amdgcn_s_memtime();
@@ -3530,6 +3538,8 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
         __syncthreads();
         const int Mc = Sb.rng[3 * STEP_MAXU + STEP_MAXU], jl = Sb.rng[4 * STEP_MAXU + 1];
         if (Mc > MC_CAP) return -3;
+        work += Mc;
+        if (work > Sb.work_cap) return -3;                 // (uniform: every thread read the same Mc)
         // run offsets: list u's points at [ro(u), ro(u + 1)) of the merge buffers
         auto ro = [&](int u) { return Sb.rng[3 * STEP_MAXU + min(u, STEP_MAXU)]; };
         SPM(21);
@@ -3705,7 +3715,7 @@ DEV int dp_steps(const StepBufs& Sb, const double* cA, const double* cC, const d
             walk([&](double, double) { ++c; });
             int o = block_excl_scan1<NT>(c, Sb.red + 16, tid, &tot);
             if (tot == 0) { res = fail; return; }          // (a zero-width domain)
-            if (tot + 1 > NP_CAP || top + tot + 1 > POOL_CAP) { res = -3; return; }
+            if (tot + 1 > NP_CAP || top + tot + 1 > Sb.pool_cap) { res = -3; return; }
             double* const OB = Sb.PB + top;
             double* const OV = Sb.PV + top;
             walk([&](double s_, double v_) { OB[o] = s_; OV[o] = v_; ++o; });
@@ -3933,7 +3943,8 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                                   reinterpret_cast<double*>(sb + nl.rl), reinterpret_cast<double*>(sb + nl.rh),
                                   reinterpret_cast<double*>(sb + nl.dlo), reinterpret_cast<double*>(sb + nl.dhi),
                                   reinterpret_cast<double*>(sb + nl.xv), reinterpret_cast<double*>(sb + nl.lt),
-                                  sb + nl.sp, nl.spb};
+                                  sb + nl.sp, nl.spb, min(POOL_CAP, max(64, a.step_pool_cap)),
+                                  a.step_work_cap > 0 ? a.step_work_cap : STEP_WORK_CAP};
                 auto steps = [&](bool feas, bool cut, double U_ = INFINITY) {
                     return dp_steps<NT>(SB, D.cA, D.cC, D.cq, H, h.S, g, x0, lo0, hi0, lo, hi, D.x, sx, sv, lane, feas, cut, U_);
                 };
@@ -3946,6 +3957,13 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 // solution rows; without one the feasibility pass (all duty costs 0: the feasible set as a few
                 // intervals, microseconds) decides whether any schedule exists and gives one
                 double ub = (chain == first_chain && (eflags & BK_OK)) ? sched_cost() : INFINITY;
+                // the bucketed schedule (x, u per stage) kept aside in the chain's battery slots (zero until
+                // the battery LP, which runs after both chains): what stands in if the DP runs out of room
+                const bool have_bk = ub < INFINITY;
+                if (have_bk) {
+                    for (int k = lane; k < H; k += NT) { D.x[k * 8 + S_CH] = D.x[k * 8 + sx]; D.x[k * 8 + S_DIS] = D.x[k * 8 + sv]; }
+                    __syncthreads();
+                }
 #ifdef DRAGG_STEP_PROF
                 unsigned long long pt = __builtin_amdgcn_s_memtime();
                 auto pmark = [&](int slot_) {
@@ -4015,10 +4033,22 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
 #ifdef DRAGG_STEP_PROF
                         if (lane == 0) D.x[17 * 8 + S_PAD] += 10.0;
 #endif
-                        // past the pool's capacity: the feasibility pass's schedule stands in (reason 6)
-                        r = steps(true, false);
+                        // past the pool's capacity or the work bound: the bucketed schedule stands in (the mid /
+                        // big launch's, a feasible schedule whose cost bounded the DP), else the feasibility
+                        // pass's; flagged approximate (reason 6)
+                        if (have_bk) {
+                            for (int k = lane; k < H; k += NT) { D.x[k * 8 + sx] = D.x[k * 8 + S_CH]; D.x[k * 8 + sv] = D.x[k * 8 + S_DIS]; }
+                            __syncthreads();
+                            r = 1;
+                        } else {
+                            r = steps(true, false);
+                        }
                         int_path |= (1 << chain) | (6 << (4 + 4 * chain));
                     }
+                }
+                if (have_bk) {
+                    for (int k = lane; k < H; k += NT) { D.x[k * 8 + S_CH] = 0.0; D.x[k * 8 + S_DIS] = 0.0; }
+                    __syncthreads();
                 }
 #undef PMARK
                 ok = r == 1;
@@ -4314,13 +4344,16 @@ constexpr int MAX_DEV = 64;
 
 // Diagnostic knobs, read once per process (not on every step): DRAGG_WAVES_PER_HOME=1|2|4 forces
 // the hot launch's waves per home (A/B runs); DRAGG_FORCE_STEP_DP=1 sends every home's chains to
-// the step-function DP (DM_NARROW).  Unset: one wave per home, the regular launch order.  (Round 4
+// the step-function DP (DM_NARROW); DRAGG_STEP_POOL_CAP / DRAGG_STEP_WORK_CAP shrink that DP's pool
+// and work bound (tests of its capacity path).  Unset: one wave per home, the regular launch order.  (Round 4
 // measured and removed a prediction of the narrow homes before the hot launch with their step-function DP
 // on a high-priority side stream beside it: 2.81 against 2.29 ms over the full day -- the side solves
 // outlast the hot launch and take CUs from it -- and ~0.1 ms of prediction per step at 1,250 homes.)
 struct Knobs {
     int waves = 1;
     int force_steps = 0;
+    int step_pool_cap = POOL_CAP;     // DRAGG_STEP_POOL_CAP: a smaller step-function DP pool (tests of its
+    long long step_work_cap = 0;      //   capacity path); DRAGG_STEP_WORK_CAP: its work bound (0: default)
 };
 Knobs read_knobs() {
     Knobs r;
@@ -4328,6 +4361,10 @@ Knobs read_knobs() {
     if (w && (w[0] == '1' || w[0] == '2' || w[0] == '4') && w[1] == 0) r.waves = w[0] - '0';
     const char* f = getenv("DRAGG_FORCE_STEP_DP");
     r.force_steps = (f && f[0] == '1') ? 1 : 0;
+    const char* pc = getenv("DRAGG_STEP_POOL_CAP");
+    if (pc && atoi(pc) > 0) r.step_pool_cap = atoi(pc);
+    const char* wc = getenv("DRAGG_STEP_WORK_CAP");
+    if (wc && atoll(wc) > 0) r.step_work_cap = atoll(wc);
     return r;
 }
 Knobs g_knobs = read_knobs();          // at library load; again only on dragg_mpc_reload_knobs()
@@ -4378,6 +4415,8 @@ int launch(const KArgs& a, hipStream_t s) {
     int* const blen = reinterpret_cast<int*>(wsb + mid_list_offset(N, a.d.horizon)) + N;
     KArgs b = a;
     b.force_steps = knobs().force_steps;
+    b.step_pool_cap = knobs().step_pool_cap;
+    b.step_work_cap = knobs().step_work_cap;
     // each list's length and the persistent launch's take counter after it, in one tiny launch
     // (three 8-byte memsets cost three fills: ~13 us of a 0.49 ms step at 1,250 homes)
     hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, nlen, blen, nullptr, nullptr);
@@ -4427,6 +4466,8 @@ int launch_lag(const KArgs& a, bool side, hipStream_t s) {
     int* const blen = reinterpret_cast<int*>(lw + mid_list_offset(N, H)) + N;
     KArgs b = a;
     b.force_steps = 0;
+    b.step_pool_cap = knobs().step_pool_cap;
+    b.step_work_cap = knobs().step_work_cap;
     const size_t lds = kernel_lds_bytes(&a.d);
     if (!side) {
         hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, blen, a.skip + N, a.nar + N, nullptr);

@@ -186,7 +186,9 @@ typedef struct dragg_mpc_out {
                                    the big launch's 2,048 labels keeps its bucketed schedule
                                    (default build; DRAGG_FLAG_EXACT sends it to the step-function
                                    DP), 6 = the exact step-function DP past its capacity (its pool
-                                   of 2^20 breakpoints per chain); bit 12 = solved by a later launch (its front
+                                   of 2^20 breakpoints per chain, or its work bound of 2 M merge
+                                   points per pass): the bucketed schedule it was handed stands in
+                                   (else the feasibility pass's); bit 12 = solved by a later launch (its front
                                    outgrew the hot launch's capacity; still exact when
                                    bits 0-11 are 0); bits 13 / 14 = status ROUND_FAIL
                                    decided by the indoor-air / tank chain (no integer duty
@@ -264,7 +266,8 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
 
 /* Diagnostic knobs, read from the environment when the library loads and again only here (never
    per step): DRAGG_WAVES_PER_HOME=1|2|4 (the hot launch's waves per home; results bit-identical) and
-   DRAGG_FORCE_STEP_DP=1 (every chain through the step-function DP; tests).  Unset: the defaults. */
+   DRAGG_FORCE_STEP_DP=1 (every chain through the step-function DP; tests), DRAGG_STEP_POOL_CAP=n and
+   DRAGG_STEP_WORK_CAP=n (a smaller pool / work bound of that DP; tests of its capacity path).  Unset: the defaults. */
 void dragg_mpc_reload_knobs(void);
 
 /* Fill `info` for these dims (needs a GPU: queries the current device). */

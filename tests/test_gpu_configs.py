@@ -258,8 +258,12 @@ def test_config4_rl_10k_homes_price_broadcast_and_rollouts(gpu):
           f"{fb.mean() if len(fb) else 0:.1e}, max {fb.max() if len(fb) else 0:.1e}")
     # under RL prices a chain past the big fronts keeps its bucketed schedule by default (the step-function
     # DP explodes on a price that changes at every stage; DRAGG_FLAG_EXACT sends it there): at most 0.1 %
-    # of the homes, each flagged in int_path with reason 3
+    # of the homes, each flagged in int_path with reason 3 on the chain that kept it
     assert n_off <= 0.001 * len(homes), n_off
+    for p_ in path[(st == 0) & (path & L.PATH_APPROX_MASK != 0)]:
+        for c in (0, 1):
+            if p_ & (1 << c):
+                assert (p_ >> (4 + 4 * c)) & 0xF == 3, hex(p_)
     _report("configs[4] RL 10k homes, H = 48, July, rollout = commit", agg, homes, [(t,) + res], min_opt=0)
 
 
@@ -353,9 +357,9 @@ def test_bench_narrow_set_solves_gap_bound_and_exact_mode(bench_day):
     front DP's dominance; the exact step-function DP (DM_NARROW, int_path bit 15) solves it, on the
     domains cut by the LP bounds and the bucketed schedule's cost.  Every such solve of the bench
     workload over 100 steps: status and objective equal to the exact optimum (oracle/thermal.py
-    exact_milp, the assumption-free backward DP; 1e-9).  MPCBatch(exact=True) (DRAGG_FLAG_EXACT, kept for
-    the ABI, no effect) gives the same: every one equals the exact optimum and none keeps an
-    approximation."""
+    exact_milp, the assumption-free backward DP; 1e-9).  MPCBatch(exact=True) (DRAGG_FLAG_EXACT: it only
+    changes RL-priced chains whose fronts pass 2,048 labels, none here) gives the same: every one equals
+    the exact optimum and none keeps an approximation."""
     import torch
     from dragg_amd import _lib as L
     from dragg_amd.aggregator import DeviceAggregator

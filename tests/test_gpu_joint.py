@@ -88,8 +88,9 @@ def test_narrow_set_solves_against_the_joint_optimum(gpu):
     """Narrow-set cases: the kernel's objective equals the exact sequential optimum (oracle/thermal.py's
     assumption-free step-function DP + the LP, 1e-9 rel), never lies below HiGHS's dual bound on the
     joint model, and equals HiGHS's joint optimum where it proved one (1e-6).  The default build takes
-    these chains to the step-function DP too (DRAGG_FLAG_EXACT is kept for ABI compatibility and changes
-    nothing): the same status, the same objective (1e-9), no chain left on an approximate schedule."""
+    these chains to the step-function DP too: DRAGG_FLAG_EXACT only matters for an RL-priced chain whose
+    front passes the big launch's 2,048 labels, and these cases are TOU-priced, so with or without it:
+    the same status, the same objective (1e-9), no chain left on an approximate schedule."""
     from dragg_amd import _lib as L
     cases = [c for c in _cases() if c["status"] != "round_fail"]
     if not cases:
