@@ -18,6 +18,7 @@
 #include <stdint.h>
 #include <limits.h>
 #include <stdlib.h>
+#include <stdio.h>
 
 #include "../../include/dragg_mi355x.h"
 
@@ -4354,6 +4355,7 @@ struct Knobs {
     int force_steps = 0;
     int step_pool_cap = POOL_CAP;     // DRAGG_STEP_POOL_CAP: a smaller step-function DP pool (tests of its
     long long step_work_cap = 0;      //   capacity path); DRAGG_STEP_WORK_CAP: its work bound (0: default)
+    int side_grid[4] = {0, 0, 0, 0};  // DRAGG_SIDE_GRID=hot,mid,big,narrow: the side pass's blocks (A/B)
 };
 Knobs read_knobs() {
     Knobs r;
@@ -4365,6 +4367,8 @@ Knobs read_knobs() {
     if (pc && atoi(pc) > 0) r.step_pool_cap = atoi(pc);
     const char* wc = getenv("DRAGG_STEP_WORK_CAP");
     if (wc && atoll(wc) > 0) r.step_work_cap = atoll(wc);
+    const char* sg = getenv("DRAGG_SIDE_GRID");
+    if (sg) sscanf(sg, "%d,%d,%d,%d", &r.side_grid[0], &r.side_grid[1], &r.side_grid[2], &r.side_grid[3]);
     return r;
 }
 Knobs g_knobs = read_knobs();          // at library load; again only on dragg_mpc_reload_knobs()
@@ -4452,8 +4456,14 @@ int launch(const KArgs& a, hipStream_t s) {
 //        per-block scratch in lag->side_workspace) and the step-function DP over lag->narrow.
 // A home's clock moves to t + 1 when its step is complete; so the next main pass solves every home
 // whose step-function DP finished in time and leaves the others to the side stream, which runs behind.
-constexpr int SIDE_HOT_BLOCKS = 256;        // persistent blocks of the side pass's hot launch
-constexpr int SIDE_NARROW_BLOCKS = 8;       // ... of its step-function launch (each needs a whole CU's LDS)
+// The side pass's persistent launches are small: it usually holds one or two lagging homes, and its
+// empty blocks run beside the main pass's next hot launch.  Measured (driver window, 20 steps): a full-
+// size side pass (256 / ~1,800 / 512 / 8 blocks) 1.482 ms/step, 16 / 16 / 16 / 2 blocks 1.434, 4 / 4 /
+// 4 / 1 1.435, serial steps 1.427; full day 1.807 / 1.759 / 1.775 ms/step
+constexpr int SIDE_HOT_BLOCKS = 16;         // persistent blocks of the side pass's hot launch
+constexpr int SIDE_MID_BLOCKS = 16;         // ... mid launch
+constexpr int SIDE_BIG_BLOCKS = 16;         // ... big launch
+constexpr int SIDE_NARROW_BLOCKS = 2;       // ... step-function launch (each needs a whole CU's LDS)
 int launch_lag(const KArgs& a, bool side, hipStream_t s) {
     static int attr_dev[MAX_DEV][8] = {};
     int dev = 0;
@@ -4488,15 +4498,17 @@ int launch_lag(const KArgs& a, bool side, hipStream_t s) {
     b.hot_list = a.skip;
     b.skip = nullptr;
     b.side = 1;
-    int rc = launch_kernel(mpc_direct_kernel<false, DM_FRONT, 1>, attr[0], b, min(N, SIDE_HOT_BLOCKS), WAVE, lds, s);
+    const int* sg = knobs().side_grid;
+    auto grid = [&](int i, int dflt) { return max(1, min(N, sg[i] > 0 ? sg[i] : dflt)); };
+    int rc = launch_kernel(mpc_direct_kernel<false, DM_FRONT, 1>, attr[0], b, grid(0, SIDE_HOT_BLOCKS), WAVE, lds, s);
     b.hot_list = nullptr;
     if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_MID, NW_MID>, attr[6], b,
-                                min(N, mid_slots<false>(dev, H, a.d.sub_steps)), NW_MID * WAVE,
+                                grid(1, SIDE_MID_BLOCKS), NW_MID * WAVE,
                                 (size_t)mid_layout(H, a.d.sub_steps).bytes, s);
-    if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_BUCKET, NW_BIG>, attr[2], b, min(N, SECOND_SLOTS),
+    if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_BUCKET, NW_BIG>, attr[2], b, grid(2, SIDE_BIG_BLOCKS),
                                 NW_BIG * WAVE, (size_t)big_layout(H, a.d.sub_steps).bytes, s);
     if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_NARROW, NT_STEPS / WAVE>, attr[5], b,
-                                min(N, SIDE_NARROW_BLOCKS), NT_STEPS, (size_t)narrow_layout(H, a.d.sub_steps).bytes, s);
+                                grid(3, SIDE_NARROW_BLOCKS), NT_STEPS, (size_t)narrow_layout(H, a.d.sub_steps).bytes, s);
     return rc;
 }
 

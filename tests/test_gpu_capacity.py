@@ -23,9 +23,10 @@ HOME, STEP = 7519, 36
 @pytest.fixture(scope="module")
 def at_step():
     dt, hh, steps = 4, 12, STEP + 1
-    days = math.ceil((math.ceil(steps / dt) + hh + 2) / 24) + 1
+    gen = 64                                    # the community and weather of tests/test_gpu_overlap.py
+    days = math.ceil((math.ceil(gen / dt) + hh + 2) / 24) + 1
     homes = synthetic_homes(10000, seed=12, days=days, dt=dt, horizon_hours=hh)
-    oat, ghi, tou = synthetic_weather(days, dt, math.ceil(steps / dt), seed=3, month=7)
+    oat, ghi, tou = synthetic_weather(days, dt, math.ceil(gen / dt), seed=3, month=7)
     agg = DeviceAggregator(homes, oat, ghi, tou, 0, steps, reward_price=[0.0], seed=12, keep_history=False)
     for _ in range(STEP):
         agg.run_iteration()
