@@ -58,6 +58,16 @@ constexpr int MC_CAP = 8 * NP_CAP;        // merged candidate points of one stag
 constexpr int STEP_CH = 8;                // merged outputs per merge work item, at most (fewer on small stages)
 constexpr int LW_ROWS = 256;              // rows of the LP bounds L_k / W_k per slot (H < LW_ROWS)
 constexpr int NF_MID = 384;              // front capacity of the mid launch (DM_MID)
+// RL-priced chains (a price change at most stages): the exact front DPs prune by a cell bound -- a lower
+// bound of the INTEGER cost-to-go per cell of a uniform grid over the chain's box (cell_rows), 1-3 %
+// below the optimum where the LP cost-to-go is ~13 % below -- and a beam pass (fronts truncated to the
+// BEAM_K labels of least cost + bound) gives the upper bound (measured on the bench's RL price, oracle
+// prototype: the beam's schedule is the optimum on 18 of 20 chains, within 0.03 % on the others; the
+// exact pass's fronts then hold 22-280 labels, where the LP bound and the bucketed schedule's cost left
+// 30 % of the chains past 2,048)
+constexpr int NCELL = 1024;              // cells of the grid
+constexpr int BEAM_K = 48;               // labels a beam stage keeps (7 BEAM_K children fit NF_MID)
+constexpr int CELL_TRIES = 8;            // bisection steps on the bound after a pass past the capacity
 constexpr int NTB_MID = 128;             // ... and its key / cost buckets per stage
 constexpr int MID_SLOTS_MAX = 2048;      // blocks of the persistent mid launch (~7 per CU at H = 48)
 // exchange area of a multi-wave front DP: per-pass survivor masks, per-wave counts / ranges / minima
@@ -1047,10 +1057,10 @@ DEV bool dp_chain(const Home& h, const Lds& L, const DpChain& c, int lane) {
     return true;
 }
 
-template <int SS, int CAP = NF, int CAPB = NF_BOUND, int PS = NB_CAP, int NBK = NTB, int NW = 1>
+template <int SS, int CAP = NF, int CAPB = NF_BOUND, int PS = NB_CAP, int NBK = NTB, int NW = 1, bool CELL = false>
 DEV int dp_front(const struct FrontBufs& B, int H, int tid, double g, double x0, double lo0, double hi0, double lo,
                  double hi, int sx, int sv, bool use_bound = false, double ub_ext = INFINITY,
-                 double* best_out = nullptr);
+                 double* best_out = nullptr, int beam_k = 0);
 
 // int_mode round_lp: the integer duties after the relaxation, by the exact front DP (the
 // default path's, dp_front) with its buffers in the KKT-factor LDS the ADMM no longer needs
@@ -1510,8 +1520,16 @@ __host__ __device__ inline size_t mid_list_offset(int N, int H) {
 __host__ __device__ inline size_t mid_region_offset(int N, int H) {
     return (mid_list_offset(N, H) + (size_t)(N + 2) * sizeof(int) + 255) / 256 * 256;
 }
-__host__ __device__ inline size_t direct_workspace_bytes(int N, int H) {
-    return mid_region_offset(N, H) + (size_t)MID_SLOTS_MAX * H * NF_MID * sizeof(uint16_t);
+// then (256-aligned), with a reward-price list (dims.n_rp > 1: RL prices possible), the cell bound's
+// rows of every home's indoor-air chain [N][H + 1][NCELL] f32 (cell_kernel; row 0, cell 0: 1 = valid)
+__host__ __device__ inline size_t cell_region_offset(int N, int H) {
+    return (mid_region_offset(N, H) + (size_t)MID_SLOTS_MAX * H * NF_MID * sizeof(uint16_t) + 255) / 256 * 256;
+}
+__host__ __device__ inline size_t cell_region_bytes(int N, int H, bool cells) {
+    return cells ? (size_t)N * (H + 1) * NCELL * sizeof(float) : 0;
+}
+__host__ __device__ inline size_t direct_workspace_bytes(int N, int H, bool cells) {
+    return cell_region_offset(N, H) + cell_region_bytes(N, H, cells);
 }
 
 struct DirectLayout {
@@ -1639,7 +1657,7 @@ __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
 // is done with them, its schedule is in the global solution array) the big exact pass's
 // fronts [NF_BIG], W table, bucket arrays and hull.
 struct BigLayout {
-    int fa, fb, wl, kb, cb, mh, kl, flo, fhi, xch, bytes;
+    int fa, fb, wl, kb, cb, mh, kl, flo, fhi, xch, cl, bytes;   // cl: the cell bound's row (mid only; -1: none)
 };
 __host__ __device__ inline BigLayout big_layout(int H, int S) {
     const DirectLayout d = direct_layout(H, S);
@@ -1657,6 +1675,7 @@ __host__ __device__ inline BigLayout big_layout(int H, int S) {
     o.fhi = take(4 * (H + 1), 4);
     p = max(p, d.bytes);                         // past the direct layout too: the regular front DP of
     o.xch = take(max(xch_bytes(NF_BIG), xch_bytes(NF)), 16);   // the (multi-wave) launch uses it as well
+    o.cl = -1;                                   // (no room for 2 blocks per CU: rows read from the workspace)
     o.bytes = (p + 15) / 16 * 16;
     return o;
 }
@@ -1679,6 +1698,7 @@ __host__ __device__ inline BigLayout mid_layout(int H, int S) {
     o.fhi = take(4 * (H + 1), 4);
     p = max(p, d.bytes);
     o.xch = take(max(xch_bytes(NF_MID), xch_bytes(NF)), 16);
+    o.cl = take(4 * NCELL, 16);
     o.bytes = (p + 15) / 16 * 16;
     return o;
 }
@@ -2344,6 +2364,10 @@ struct FrontBufs {
                                          //   +inf padded; nullptr = no bound pruning
     double *wlx, *wlv, *wls;             // [WAVE] LDS: the current stage's W (points, slopes)
     char* xch;                           // [xch_bytes(CAP)] LDS: the waves' exchange area (NW > 1)
+    // dp_front<..., CELL = true>: the cell bound in place of W
+    const float* cg;                     // [H + 1][NCELL] global: cell_rows' lower bounds of x_k's cost-to-go
+    float* cl;                           // [NCELL] LDS: the current stage's row
+    double c_lo, c_inv;                  // the grid: cell of x = floor((x - c_lo) c_inv)
 };
 
 // 1 / w to about 1 ulp: v_rcp_f64 and one Newton step (no IEEE division sequence)
@@ -2399,9 +2423,100 @@ DEV T dpp_iscan(T v, int lane, T id, Op op) {
     return row == 0 ? v : op(v, off);
 }
 
-template <int SS, int CAP, int CAPB, int PS, int NBK, int NW>
+// The cell bound of one chain: row k of cg (k = 1 .. H) holds, per cell [a, b] of a uniform grid of
+// NCELL cells over the chain's box, a LOWER bound of the integer cost-to-go of every state x_k in the
+// cell (widened by rounding margins): row H = 0 on the cells meeting x_H's box, and row k = min over
+// the duties u of q_k u + min of row k + 1 over the cells the image A [a, b] + C + g u meets inside
+// x_{k+1}'s box (+inf where none) -- a minimum over a superset of the states a schedule can reach,
+// rounded down to f32.  r0 / r1: two LDS rows of scratch.  Every thread of the block calls it; false
+// (no bound) on a degenerate stage (A <= 0).
+// the cell grid over a chain's box [bl, bh] (widened past every tolerance of the labels' box tests)
+DEV void cell_grid(double bl, double bh, double& c_lo, double& c_inv) {
+    auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
+    c_lo = bl - 8.0 * tw(bl);
+    c_inv = (double)NCELL / ((bh + 8.0 * tw(bh)) - c_lo);
+}
+
+template <int NT, int SS>
+DEV bool cell_rows(float* cg, float* r0, float* r1, const double* cA, const double* cC, const double* cq, int H, int S,
+                   double g, double lo0, double hi0, double lo, double hi, double c_lo, double c_inv, int tid) {
+    auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
+    const double dlt = 1.0 / c_inv;
+    const double eps = 16.0 * TOL_P * (1.0 + fabs(c_lo) + NCELL * dlt);     // past the cell lookup's rounding
+    auto bxl = [&](int k) { const double b = k <= 1 ? lo0 : lo; return b - tw(b); };   // box of x_k
+    auto bxh = [&](int k) { const double b = k <= 1 ? hi0 : hi; return b + tw(b); };
+    for (int k = 0; k < H; ++k)
+        if (!(cA[k] > 0.0)) return false;                  // (uniform)
+    // cells meeting a box [l, h]: [cell(l - eps), cell(h + eps)] (clamped to the grid)
+    auto cell_span = [&](double l, double h, int& c0, int& c1) {
+        c0 = max(0, (int)floor((l - eps - c_lo) * c_inv));
+        c1 = min(NCELL - 1, (int)floor((h + eps - c_lo) * c_inv));
+    };
+    {
+        int c0, c1;
+        cell_span(bxl(H), bxh(H), c0, c1);
+        for (int j = tid; j < NCELL; j += NT) {
+            const float v = (j >= c0 && j <= c1) ? 0.0f : INFINITY;
+            r0[j] = v;
+            cg[(size_t)H * NCELL + j] = v;
+        }
+    }
+    __syncthreads();
+    float* nxt = r0;
+    float* cur = r1;
+    for (int k = H - 1; k >= 1; --k) {
+        const double A = cA[k], C = cC[k], q = cq[k];
+        int b0, b1;
+        cell_span(bxl(k), bxh(k), b0, b1);
+        // the image of cell j = [a_j - eps, b_j + eps] under duty u, in cell units of x_{k+1}: its ends are
+        // affine in j (slope A), lo_u + j A and lo_u + (j + 1) A + w; widened by a margin far above the
+        // rounding of this form (1e-6 cells) and of the labels' own arithmetic (tw) -- a superset of the
+        // cells the states of cell j reach (outside the grid: clamped, where no state stays feasible)
+        const double mg = 1e-6 + (2.0 * tw(fabs(C) + fabs(A) * (fabs(c_lo) + NCELL * dlt) + fabs(g) * S) + eps) * c_inv;
+        const double base = (fma(A, c_lo - eps, C) - c_lo) * c_inv - mg;       // lo_0 at j = 0 (u = 0)
+        const double wd = 2.0 * (A * eps * c_inv + mg);                          // the image's extra width
+        const double gu = g * c_inv;
+        for (int j = tid; j < NCELL; j += NT) {
+            double best = INFINITY;
+            if (j >= b0 && j <= b1) {
+                const double lj = fma((double)j, A, base);
+                // every duty's (one or two) loads issued together: clamped indices, the test after
+                float m0[SS + 1], m1[SS + 1];
+                int span[SS + 1];
+#pragma unroll
+                for (int u = 0; u <= SS; ++u) {
+                    const double l = fma((double)u, gu, lj), h = l + A + wd;
+                    const bool in = h >= 0.0 && l <= (double)NCELL;
+                    const int i0 = in ? min(NCELL - 1, max(0, (int)floor(l))) : 0;
+                    const int i1 = in ? min(NCELL - 1, max(i0, (int)floor(h))) : 0;
+                    m0[u] = nxt[i0];
+                    m1[u] = nxt[min(i0 + 1, i1)];
+                    span[u] = in ? i1 - i0 : -1;
+                }
+#pragma unroll
+                for (int u = 0; u <= SS; ++u) {
+                    if (span[u] < 0) continue;
+                    float m = fminf(m0[u], m1[u]);
+                    if (span[u] > 1) {                     // (a stage with A > 1: a wider image)
+                        const int i0 = min(NCELL - 1, max(0, (int)floor(fma((double)u, gu, lj))));
+                        for (int i = i0 + 2; i <= i0 + span[u]; ++i) m = fminf(m, nxt[i]);
+                    }
+                    if (m < INFINITY) best = fmin(best, fma(q, (double)u, (double)m));
+                }
+            }
+            const float v = best < INFINITY ? __double2float_rd(best) : INFINITY;
+            cur[j] = v;
+            cg[(size_t)k * NCELL + j] = v;
+        }
+        __syncthreads();
+        float* t_ = nxt; nxt = cur; cur = t_;
+    }
+    return true;
+}
+
+template <int SS, int CAP, int CAPB, int PS, int NBK, int NW, bool CELL>
 DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double lo0, double hi0, double lo,
-                 double hi, int sx, int sv, bool use_bound, double ub_ext, double* best_out) {
+                 double hi, int sx, int sv, bool use_bound, double ub_ext, double* best_out, int beam_k) {
     // NW waves share one home's DP (latency: few homes per GPU): every wave runs the same
     // uniform control flow (W table, hulls and scans are computed redundantly or by wave 0), the
     // children of a stage are split into contiguous pass ranges per wave, and survivors keep the
@@ -2599,10 +2714,34 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
 #endif
         return prune;
     };
-    bool prune = B.wg != nullptr && (use_bound || nodom) && make_bound(0, x0, 0.0);
-    if (nodom && !prune) return nodom && (pos && neg) ? -1 : -2;
+    bool prune;
+    if constexpr (CELL) {
+        // the cell bound (B.cg) prunes from stage 0 on against the caller's upper bound; a beam pass
+        // (beam_k > 0) runs without one: its truncation keeps the fronts small, with or without dominance
+        double qabs = 0.0;
+        for (int k = lane; k < H; k += WAVE) qabs += fabs(B.cq[k]) * SS;
+        qabs = dpp_sum(qabs);
+        prune = ub_ext < INFINITY;
+        if (prune) UBT = ub_ext + TOL_P * (1.0 + fabs(ub_ext) + qabs);
+        if (nodom && !prune && beam_k == 0) return (pos && neg) ? -1 : -2;
+    } else {
+        prune = B.wg != nullptr && (use_bound || nodom) && make_bound(0, x0, 0.0);
+        if (nodom && !prune) return nodom && (pos && neg) ? -1 : -2;
+    }
     int capn = prune ? CAPB : CAP;                   // front capacity (overflow: -3)
-    bool tried = prune || B.wg == nullptr;           // the bound is built at most once
+    bool tried = CELL || prune || B.wg == nullptr;   // the bound is built at most once
+    // the cell bound's row of the stage's children (LDS) and the next row in flight (registers)
+    constexpr int CPL = CELL ? NCELL / NT : 1;
+    float cpre[CPL];
+    // (B.cl == nullptr: the rows are read from the workspace -- the big launch, whose LDS has no room)
+    const float* crow = B.cl ? B.cl : B.cg + NCELL;
+    auto cell_at = [&](double x) -> double {
+        const int c = min(NCELL - 1, max(0, (int)floor((x - B.c_lo) * B.c_inv)));
+        return (double)crow[c];
+    };
+    auto bound_at = [&](double x, int wst_) -> double {
+        if constexpr (CELL) return cell_at(x); else return w_eval(B, x, wst_);
+    };
     // the front stores each label's exact STATE x (not its key dx * x) and cost
     double2* fa = B.fa;
     double2* fb = B.fb;
@@ -2613,7 +2752,15 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     for (int b = tid; b < NBK; b += NT) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
     // W_{k+1} of the stage in the LDS table, W_{k+2} in flight
     double2 wnext = make_double2(INFINITY, INFINITY);
-    if (prune && wid == 0) {
+    if constexpr (CELL) {
+        if (B.cl) {
+#pragma unroll
+            for (int j = 0; j < CPL; ++j) {
+                B.cl[j * NT + tid] = B.cg[(size_t)1 * NCELL + j * NT + tid];
+                cpre[j] = H >= 2 ? B.cg[(size_t)2 * NCELL + j * NT + tid] : 0.0f;
+            }
+        }
+    } else if (prune && wid == 0) {
         const double2 w1 = load_row(1);
         w_to_lds(B, lane, w1.x, w1.y);
         if (H >= 2) wnext = load_row(2);
@@ -2686,7 +2833,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             bl = fmax(bl, fma((double)B.flo[k + 1], hs, hb));
             bh = fmin(bh, fma((double)B.fhi[k + 1], hs, hb));
         }
-        const int wst = prune ? w_st0(row_m(k + 1)) : 0;   // W_{k+1}'s search depth
+        const int wst = (prune && !CELL) ? w_st0(row_m(k + 1)) : 0;   // W_{k+1}'s search depth
         // the children's state and cost ranges (widened past rounding) define the two bucket
         // grids of this stage.  A child's position in a range as a 32-bit fixed-point number
         // v = (key - lo) * NBK * 2^23 / (hi - lo) (one fma from the state) gives its bucket
@@ -2722,7 +2869,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             const double2 Li = fa[i];
             const double xc = fma(A, Li.x, fma(g, (double)u, C));
             const double cc = fma(q, (double)u, Li.y);
-            if (xc >= bl && xc <= bh && (!prune || cc + w_eval(B, xc, wst) <= UBT)) {
+            if (xc >= bl && xc <= bh && (!prune || cc + bound_at(xc, wst) <= UBT)) {
                 const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
                 const unsigned cu = vc + 2u, kd = dn(vk);
                 atomicMin(&B.kb[min(NBK - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
@@ -2787,7 +2934,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             vk = fixp(fma(xc, kmul, kadd));
             vc = fixp(fma(cc, csc, cadd));
             bool keep = have && xc >= bl && xc <= bh;
-            if (keep && prune) keep = cc + w_eval(B, xc, wst) <= UBT;
+            if (keep && prune) keep = cc + bound_at(xc, wst) <= UBT;
             if (keep && !nodom) {
                 const int kbk = min(NBK - 1, (int)(vk >> 23)), cbk = min(NBK - 1, (int)(vc >> 23));
                 const unsigned ku = vk + 2u, cd = dn(vc);
@@ -2874,6 +3021,88 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                                             (k == 0 ? (prune ? 1e8 : 0.0) * (sx == S_T ? 1.0 : 2.0) : 0.0);
 #endif
         if (nn == 0) return 0;                       // no child left inside the feasible set
+        if constexpr (CELL && NW == 1) {
+            // beam: keep the beam_k labels of least cost + bound (index order inside the threshold's
+            // bucket), the threshold by two histogram levels; in-order compaction chunk by chunk (a label
+            // only moves down), its back-pointer with it
+            if (beam_k > 0 && nn > beam_k && nn <= capn) {
+                double fl = INFINITY, fh = -INFINITY;
+                for (int i = lane; i < nn; i += WAVE) {
+                    const double2 Li = fb[i];
+                    const double f = Li.y + cell_at(Li.x);
+                    fl = fmin(fl, f); fh = fmax(fh, f);
+                }
+                fl = dpp_reduce(fl, [](double a_, double b_) { return fmin(a_, b_); });
+                fh = dpp_reduce(fh, [](double a_, double b_) { return fmax(a_, b_); });
+                // the threshold by two histograms of 64 buckets (LDS atomics): over [fl, fh], then over the
+                // bucket in which the count of labels below reaches beam_k
+                int* const hl = reinterpret_cast<int*>(B.xch);      // (one wave: the exchange area is free)
+                double bl_ = fl, bsc = fh > fl ? 64.0 / (fh - fl) : 0.0;
+                auto bucket_of = [&](double f, double b0_, double sc_) {
+                    return f < INFINITY ? min(63, max(0, (int)((f - b0_) * sc_))) : 64;
+                };
+                int need = beam_k;                         // labels still to keep at the current level
+                double thr_lo = -INFINITY;                  // labels with f < thr_lo are kept
+                double thr_in = INFINITY, fcut = INFINITY;  // finally: keep f < thr_in, and of [thr_in, fcut)
+                int need_in = 0;                            //   the first need_in in index order
+                for (int lvl = 0; lvl < 2; ++lvl) {
+                    hl[lane] = 0;
+                    wave_sync();
+                    for (int i = lane; i < nn; i += WAVE) {
+                        const double f = fb[i].y + cell_at(fb[i].x);
+                        if (f >= thr_lo && (lvl == 0 || f < bl_ + 64.0 / bsc)) {
+                            const int bk = bucket_of(f, bl_, bsc);
+                            if (bk < 64) atomicAdd(hl + bk, 1);
+                        }
+                    }
+                    wave_sync();
+                    const int cnt_ = hl[lane];
+                    const int incl = dpp_iscan(cnt_, lane, 0, [](int a_, int b_) { return a_ + b_; });
+                    const int bs = __ffsll((long long)__ballot(incl >= need)) - 1;
+                    wave_sync();
+                    if (bs < 0 || bsc == 0.0) {                // (fewer finite labels than needed, or one f)
+                        thr_in = INFINITY; fcut = INFINITY; need_in = 0;
+                        if (bsc == 0.0 && bs >= 0) { thr_in = fl; fcut = INFINITY; need_in = need; }
+                        break;
+                    }
+                    const int below_bs = read_lane(incl, bs) - read_lane(cnt_, bs);
+                    thr_in = bl_ + bs / bsc;
+                    fcut = bl_ + (bs + 1) / bsc;
+                    need_in = need - below_bs;
+                    if (lvl == 1) break;
+                    // keep the buckets below bs; refine inside bs
+                    need = need_in;
+                    thr_lo = thr_in;
+                    bl_ = thr_in;
+                    bsc *= 64.0;
+                }
+                int kept = 0, nin = 0;
+                for (int i0 = 0; i0 < nn; i0 += WAVE) {
+                    const int i = i0 + lane;
+                    double2 Li = make_double2(0.0, 0.0);
+                    uint16_t pr = 0;
+                    bool must = false, cand = false;
+                    if (i < nn) {
+                        Li = fb[i];
+                        pr = B.par[k * PS + i];
+                        const double f = Li.y + cell_at(Li.x);
+                        must = f < thr_in;
+                        cand = !must && f < fcut;
+                    }
+                    const unsigned long long bc = __ballot(cand);
+                    const bool keep_ = must || (cand && nin + __popcll(bc & below) < need_in);
+                    nin += __popcll(bc);
+                    const unsigned long long bal = __ballot(keep_);
+                    const int pos_ = kept + __popcll(bal & below);
+                    kept += __popcll(bal);
+                    if (keep_ && pos_ < beam_k) {
+                        fb[pos_] = Li;
+                        B.par[k * PS + pos_] = pr;
+                    }
+                }
+                nn = min(kept, beam_k);
+            }
+        }
         if (nn > capn) return -3;                    // front overflow
 #ifdef DRAGG_STAGE_PROF
         SP_MARK(3);
@@ -2894,7 +3123,17 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             cmax = c2 + tw(c2);
         }
         for (int b = tid; b < NBK && !nodom; b += NT) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
-        if (prune && k + 1 < H && wid == 0) {
+        if constexpr (CELL) {
+            if (B.cl == nullptr) {
+                crow = B.cg + (size_t)(k + 2) * NCELL;
+            } else if (k + 2 <= H) {
+#pragma unroll
+                for (int j = 0; j < CPL; ++j) {
+                    B.cl[j * NT + tid] = cpre[j];
+                    if (k + 3 <= H) cpre[j] = B.cg[(size_t)(k + 3) * NCELL + j * NT + tid];
+                }
+            }
+        } else if (prune && k + 1 < H && wid == 0) {
             w_to_lds(B, lane, wnext.x, wnext.y);
             if (k + 3 <= H) wnext = load_row(k + 3);
         }
@@ -2967,6 +3206,7 @@ DEV bool round_duties(const Home& h, const Lds& L, int lane, uint16_t* par) {
     B.cA = cA; B.cC = cC; B.cq = cq; B.x = L.x; B.par = par;
     B.wg = nullptr; B.wlx = B.wlv = B.wls = nullptr;     // no bound pruning on this path
     B.xch = nullptr;                                     // one wave
+    B.cg = nullptr; B.cl = nullptr; B.c_lo = 0.0; B.c_inv = 0.0;
     const bool front = h.S == 6 && par != nullptr && (f - L.Lf) <= 128 * H;
     for (int k = lane; k < H; k += WAVE) {
         cA[k] = h.aT;
@@ -3820,6 +4060,7 @@ enum DirectMode { DM_FRONT = 0, DM_BUCKET = 1, DM_NARROW = 2, DM_MID = 3 };
 constexpr int HOME_MASK = 0x0FFFFFFF;
 constexpr int BK_OK = 1 << 28;           // the bucketed DP found a schedule (in the solution rows)
 constexpr int BK_DONE = 1 << 29;         // the bucketed DP already ran for the deferred chain (mid -> big)
+constexpr int BK_BEAM = (int)(1u << 31); // ... and that schedule is the beam pass's (diagnostic: int_path bit 17)
 
 template <bool EXPLICIT, int MODE, int NW = 1>
 DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int first_chain, int eflags = 0) {
@@ -4087,51 +4328,115 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 return;
             } else {
                 pf.mark(DRAGG_PH_INTEGER);
-                // a chain the mid launch handed over: its bucketed schedule is in the solution rows
-                // already (the mid pass overflowed without writing them), only the big pass is left
-                if (SECOND && chain == first_chain && (eflags & BK_DONE))
+                const BigLayout bl = MODE == DM_MID ? mid_layout(H, a.d.sub_steps) : big_layout(H, a.d.sub_steps);
+                char* const sb = reinterpret_cast<char*>(smem);
+                double* const wl = reinterpret_cast<double*>(sb + bl.wl);
+                uint16_t* const bpar = MODE == DM_MID
+                    ? reinterpret_cast<uint16_t*>(lw + mid_region_offset(N, H)) + (size_t)slot * H * NF_MID
+                    : reinterpret_cast<uint16_t*>(lw + big_region_offset(N, H)) + (size_t)slot * H * NF_BIG;
+                // RL prices: the cell bound of the indoor-air chain (cell_kernel's rows of this home, before the
+                // mid launch); the tank chain keeps the LP bound (its fronts stay small under RL prices)
+                float* const cg = reinterpret_cast<float*>(ws + cell_region_offset(N, H)) + (size_t)home * (H + 1) * NCELL;
+                double c_lo = 0.0, c_inv = 0.0;
+                const bool have_cells = SECOND && rl_prices && h.S == 6 && chain == 0 && a.d.n_rp > 1 && cg[0] == 1.0f;
+                if (have_cells) cell_grid(fmin(lo0, lo), fmax(hi0, hi), c_lo, c_inv);
+                const FrontBufs FB{reinterpret_cast<double2*>(sb + bl.fa), reinterpret_cast<double2*>(sb + bl.fb),
+                                   reinterpret_cast<unsigned long long*>(sb + bl.kb),
+                                   reinterpret_cast<unsigned long long*>(sb + bl.cb),
+                                   reinterpret_cast<unsigned*>(sb + bl.mh), reinterpret_cast<unsigned*>(sb + bl.kl),
+                                   reinterpret_cast<unsigned*>(sb + bl.flo), reinterpret_cast<unsigned*>(sb + bl.fhi),
+                                   D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE,
+                                   sb + bl.xch, cg, bl.cl >= 0 ? reinterpret_cast<float*>(sb + bl.cl) : nullptr,
+                                   c_lo, c_inv};
+                // a chain the mid launch handed over: its upper-bound schedule (the beam's or the bucketed
+                // DP's) is in the solution rows already (the mid pass overflowed without writing them),
+                // only the big pass is left
+                bool beam_ub = false;
+                if (have_cells) int_path |= 1 << 16;       // (diagnostic bits 16-18: cell bound, beam bound, big launch)
+                if (MODE == DM_BUCKET) int_path |= 1 << 18;
+                if (SECOND && chain == first_chain && (eflags & BK_DONE)) {
                     ok = (eflags & BK_OK) != 0;
-                else
-                    ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
-                                  : dp_thermal<0>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
-                pf.mark(DRAGG_PH_ITER);                   // (round: the bucketed DP)
+                    beam_ub = (eflags & BK_BEAM) != 0;
+                } else {
+                    // the upper bound's schedule: under RL prices the beam pass (fronts cut to the BEAM_K
+                    // labels of least cost + cell bound), else / failing that the bucketed DP
+                    int rb = -1;
+                    if constexpr (MODE == DM_MID) {
+                        if (have_cells) {
+                            __syncthreads();
+                            rb = dp_front<6, NF_MID, NF_MID, NF_MID, NTB_MID, NW, true>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx,
+                                                                                    sv, false, INFINITY, nullptr, BEAM_K);
+                        }
+                    }
+                    ok = rb == 1;
+                    beam_ub = ok;
+                    if (!ok)
+                        ok = h.S == 6 ? dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv)
+                                      : dp_thermal<0>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
+                }
+                if (beam_ub) int_path |= 1 << 17;
+                pf.mark(DRAGG_PH_ITER);                   // (round: the bucketed DP / the beam)
                 int r2 = r;
                 // the big pass, except for a feasible set narrower than one duty step (no
                 // dominance there: its fronts outgrow any capacity, measured)
                 if (h.S == 6 && r != -2) {
-                    // the exact pass with big fronts, bounded by the bucketed schedule's cost
+                    // the exact pass with big fronts, bounded by the schedule's cost
                     double ub = INFINITY;
                     if (ok) {                              // (every wave sums all stages)
                         double c = 0.0;
                         for (int k = lane & (WAVE - 1); k < H; k += WAVE) c += D.cq[k] * D.x[k * 8 + sv];
                         ub = dpp_sum(c);
                     }
-                    const BigLayout bl = MODE == DM_MID ? mid_layout(H, a.d.sub_steps) : big_layout(H, a.d.sub_steps);
-                    char* const sb = reinterpret_cast<char*>(smem);
-                    double* const wl = reinterpret_cast<double*>(sb + bl.wl);
-                    uint16_t* const bpar = MODE == DM_MID
-                        ? reinterpret_cast<uint16_t*>(lw + mid_region_offset(N, H)) + (size_t)slot * H * NF_MID
-                        : reinterpret_cast<uint16_t*>(lw + big_region_offset(N, H)) + (size_t)slot * H * NF_BIG;
-                    const FrontBufs FB{reinterpret_cast<double2*>(sb + bl.fa), reinterpret_cast<double2*>(sb + bl.fb),
-                                       reinterpret_cast<unsigned long long*>(sb + bl.kb),
-                                       reinterpret_cast<unsigned long long*>(sb + bl.cb),
-                                       reinterpret_cast<unsigned*>(sb + bl.mh), reinterpret_cast<unsigned*>(sb + bl.kl),
-                                       reinterpret_cast<unsigned*>(sb + bl.flo), reinterpret_cast<unsigned*>(sb + bl.fhi),
-                                       D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE,
-                                       sb + bl.xch};
                     __syncthreads();
-                    // keeps the bucketed schedule in D.x unless it finds (and writes) the optimum
-                    if constexpr (MODE == DM_MID)
+                    // keeps the schedule in D.x unless it finds (and writes) the optimum
+                    auto cell_pass = [&](double U) {
+                        if constexpr (MODE == DM_MID)
+                            return dp_front<6, NF_MID, NF_MID, NF_MID, NTB_MID, NW, true>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, U);
+                        else
+                            return dp_front<6, NF_BIG, NF_BIG, NF_BIG, NTB_BIG, NW, true>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, U);
+                    };
+                    if (have_cells) {
+                        r2 = cell_pass(ub);
+                        // past the capacity at the schedule's cost (its slack over the optimum lets too many
+                        // labels through): bisection on the bound between the cell bound at x0 and that cost.
+                        // A pass at U >= the optimum returns the optimum (every label of an optimal schedule
+                        // passes cost + bound <= U); one below it finds no schedule (0)
+                        if (r2 == -3 && ok) {
+                            double lo_u = INFINITY;
+                            {
+                                const int u = lane & (WAVE - 1);
+                                double v = INFINITY;
+                                if (u <= 6) {
+                                    const double x1 = fma(D.cA[0], x0, fma(g, (double)u, D.cC[0]));
+                                    const double tl = lo0 - TOL_P * (1 + fabs(lo0)), th = hi0 + TOL_P * (1 + fabs(hi0));
+                                    if (x1 >= tl && x1 <= th)
+                                        v = fma(D.cq[0], (double)u,
+                                                (double)cg[NCELL + min(NCELL - 1, max(0, (int)floor((x1 - c_lo) * c_inv)))]);
+                                }
+                                lo_u = dpp_reduce(v, [](double a_, double b_) { return fmin(a_, b_); });
+                            }
+                            double hi_u = ub;
+                            for (int tr = 0; tr < CELL_TRIES && r2 == -3 && lo_u < hi_u; ++tr) {
+                                const double U = 0.5 * (lo_u + hi_u);
+                                if (!(U > lo_u && U < hi_u)) break;
+                                __syncthreads();
+                                r2 = cell_pass(U);
+                                if (r2 == 0) { lo_u = U; r2 = -3; }       // the optimum is above U
+                                else if (r2 == -3) hi_u = U;              // still too many labels
+                            }
+                        }
+                    } else if constexpr (MODE == DM_MID) {
                         r2 = dp_front<6, NF_MID, NF_MID, NF_MID, NTB_MID, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
-                    else
+                    } else {
                         r2 = dp_front<6, NF_BIG, NF_BIG, NF_BIG, NTB_BIG, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, true, ub);
+                    }
                     pf.mark(DRAGG_PH_POLISH);             // (round: the mid / big exact pass)
                     if (MODE == DM_MID && r2 == -3) {         // past NF_MID: the big launch's 2,048-label fronts
                         // (an RL-priced chain went straight to the bucketed DP: the big launch reuses
                         // its schedule; other chains ran the regular front DP first and start over)
                         if (lane == 0)
                             blist[atomicAdd(blist + N, 1)] = home | (chain << 30) |
-                                                             (rl_prices ? BK_DONE | (ok ? BK_OK : 0) : 0);
+                                                             (rl_prices ? BK_DONE | (ok ? BK_OK : 0) | (beam_ub ? BK_BEAM : 0) : 0);
                         return;
                     }
                     if (r2 == 1) ok = true;
@@ -4198,7 +4503,7 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
     char* const ws = a.lws ? a.lws : reinterpret_cast<char*>(a.p.workspace);
     const int N = a.d.n_homes, H = a.d.horizon;
     __shared__ int take;
-    if (MODE == DM_FRONT && !a.hot_list) {
+    if constexpr (MODE == DM_FRONT) {           // (the side pass's hot launch: side_front_kernel)
         const int home = blockIdx.x;
         if (home >= N) return;
         if (a.clk) {
@@ -4221,14 +4526,79 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
     // b); blocks past the list's length leave at once, every block reaches its end and exits
     const size_t lo = MODE == DM_MID ? defer_offset(N, H) : MODE == DM_BUCKET ? mid_list_offset(N, H)
                     : narrow_list_offset(N, H);
-    // (the side pass's hot launch: the skipped homes; both passes' DM_NARROW in lag mode: the step's list)
-    int* const list = MODE == DM_FRONT ? a.hot_list : (MODE == DM_NARROW && a.nar) ? a.nar
-                    : reinterpret_cast<int*>(ws + lo);
+    // (both passes' DM_NARROW in lag mode: the step's own list)
+    int* const list = (MODE == DM_NARROW && a.nar) ? a.nar : reinterpret_cast<int*>(ws + lo);
     const int cnt = min(list[N], N);
     for (int j = blockIdx.x; j < cnt;) {
         const int e = list[j];                      // home | flags | deferred chain << 30
         const int home = e & HOME_MASK, chain = (e >> 30) & 1;
-        if (home < N) solve_direct<EXPLICIT, MODE, NW>(a, home, smem, blockIdx.x, chain, e & (BK_DONE | BK_OK));
+        if (home < N) solve_direct<EXPLICIT, MODE, NW>(a, home, smem, blockIdx.x, chain, e & (BK_DONE | BK_OK | BK_BEAM));
+        __syncthreads();
+        if (threadIdx.x == 0) take = (int)gridDim.x + atomicAdd(list + N + 1, 1);
+        __syncthreads();
+        j = take;
+    }
+}
+
+// The cell bound rows of the indoor-air chain of every RL-priced home the hot launch deferred (its list,
+// before the mid launch reads it): the step's inputs as the solve derives them (prologue), the chain's
+// coefficients, cell_rows.  Blocks take the list entries by a static stride (the list's take counter is
+// the mid launch's).
+constexpr int NT_CELL = 256;
+constexpr int CELL_BLOCKS = 1024;           // blocks of the cell kernel (4 per CU)
+__host__ __device__ inline int cell_lds_bytes(int H) { return (front_layout(H).bytes + 15) / 16 * 16 + 2 * NCELL * 4; }
+__global__ __launch_bounds__(NT_CELL) void cell_kernel(KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int N = a.d.n_homes, H = a.d.horizon;
+    const int tid = threadIdx.x;
+    char* const ws = reinterpret_cast<char*>(a.p.workspace);
+    char* const lw = a.lws ? a.lws : ws;
+    const int* const list = reinterpret_cast<const int*>(lw + defer_offset(N, H));
+    const int cnt = min(list[N], N);
+    float* const r0 = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + (front_layout(H).bytes + 15) / 16 * 16);
+    float* const r1 = r0 + NCELL;
+    for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
+        const int e = list[j];
+        const int home = e & HOME_MASK;
+        if (home >= N || ((e >> 30) & 1) != 0) continue;        // (uniform; chain 0 entries only)
+        Home h;
+        LdsD D = carve_front(smem, H);
+        Lds L = lp_view(D);
+        Io io{a.vals, a.fc, N, home};
+        __syncthreads();
+        if (prologue<false>(a, h, L, io, tid, NT_CELL, D.sc) == DRAGG_ST_ERR_MISSING) continue;
+        derive(h);
+        int changes = 0;
+        for (int k = tid & (WAVE - 1); k < H; k += WAVE) changes += (k > 0 && D.price[k] != D.price[k - 1]) ? 1 : 0;
+        changes = dpp_isum(changes);
+        if (!(changes * 4 > H) || h.S != 6) continue;             // not RL-priced: the mid launch's regular path
+        for (int k = tid; k < H; k += NT_CELL) {                  // the indoor-air chain (solve_direct, chain 0)
+            const double wk = pow(h.gamma, (double)k) * D.price[k];
+            D.cA[k] = h.aT;
+            D.cC[k] = D.oat[k + 1] * h.iR * 3600 * h.inv_c;
+            D.cq[k] = wk * h.Pact;
+        }
+        __syncthreads();
+        double c_lo, c_inv;
+        cell_grid(h.Tmin, h.Tmax, c_lo, c_inv);
+        float* const cg = reinterpret_cast<float*>(ws + cell_region_offset(N, H)) + (size_t)home * (H + 1) * NCELL;
+        const bool ok = cell_rows<NT_CELL, 6>(cg, r0, r1, D.cA, D.cC, D.cq, H, 6, h.g, h.Tmin, h.Tmax, h.Tmin, h.Tmax,
+                                              c_lo, c_inv, tid);
+        if (tid == 0) cg[0] = ok ? 1.0f : 0.0f;
+    }
+}
+
+// lag mode, the side pass's hot launch: a persistent consumer of the homes the main pass skipped (its own
+// kernel, so that the main pass's hot kernel keeps its registers: one inlined solve, no list loop)
+__global__ __launch_bounds__(WAVE, 3) void side_front_kernel(KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int N = a.d.n_homes;
+    int* const list = a.hot_list;
+    const int cnt = min(list[N], N);
+    __shared__ int take;
+    for (int j = blockIdx.x; j < cnt;) {
+        const int home = list[j] & HOME_MASK;
+        if (home < N) solve_direct<false, DM_FRONT, 1>(a, home, smem, blockIdx.x, 0, 0);
         __syncthreads();
         if (threadIdx.x == 0) take = (int)gridDim.x + atomicAdd(list + N + 1, 1);
         __syncthreads();
@@ -4301,7 +4671,7 @@ size_t workspace_bytes(const dragg_mpc_dims* d) {
     // deferred homes, [N][H+1][64] LP cost-to-go rows, the second launch's [SECOND_SLOTS][H][NF_BIG]
     // u16 back-pointers; round_lp: the back-pointers of its front DP
     if (d->int_mode == DRAGG_INT_ROUND_LP) return par_region_bytes(d->n_homes, d->horizon);
-    return direct_mode(d) ? direct_workspace_bytes(d->n_homes, d->horizon) : 0;
+    return direct_mode(d) ? direct_workspace_bytes(d->n_homes, d->horizon, d->n_rp > 1) : 0;
 }
 
 // per home, the hot launch's (int_mode round: DM_FRONT)
@@ -4432,6 +4802,12 @@ int launch(const KArgs& a, hipStream_t s) {
                  : nw == 2 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>, attr[3], b, N, 2 * WAVE, lds, s)
                            : launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 1>, attr[1], b, N, WAVE, lds, s);
     if (rc) return rc;
+    // RL prices possible (a reward-price list): the cell bound of the deferred homes' indoor-air chains
+    if (a.d.n_rp > 1) {
+        const int rcc = launch_kernel(cell_kernel, attr[7], b, min(N, CELL_BLOCKS), NT_CELL,
+                                      (size_t)cell_lds_bytes(a.d.horizon), s);
+        if (rcc) return rcc;
+    }
     // the deferred homes: the mid launch (fronts of 384 labels, many blocks), its overflows to the
     // big launch (2,048 labels, 2 blocks per CU), what no front DP can take to the step-function DP
     const int rcm = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_MID, NW_MID>, attr[6], b,
@@ -4485,6 +4861,8 @@ int launch_lag(const KArgs& a, bool side, hipStream_t s) {
         b.hot_list = nullptr;
         b.side = 0;
         int rc = launch_kernel(mpc_direct_kernel<false, DM_FRONT, 1>, attr[1], b, N, WAVE, lds, s);
+        if (!rc && a.d.n_rp > 1)
+            rc = launch_kernel(cell_kernel, attr[7], b, min(N, CELL_BLOCKS), NT_CELL, (size_t)cell_lds_bytes(H), s);
         if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_MID, NW_MID>, attr[6], b,
                                     min(N, mid_slots<false>(dev, H, a.d.sub_steps)), NW_MID * WAVE,
                                     (size_t)mid_layout(H, a.d.sub_steps).bytes, s);
@@ -4500,8 +4878,10 @@ int launch_lag(const KArgs& a, bool side, hipStream_t s) {
     b.side = 1;
     const int* sg = knobs().side_grid;
     auto grid = [&](int i, int dflt) { return max(1, min(N, sg[i] > 0 ? sg[i] : dflt)); };
-    int rc = launch_kernel(mpc_direct_kernel<false, DM_FRONT, 1>, attr[0], b, grid(0, SIDE_HOT_BLOCKS), WAVE, lds, s);
+    int rc = launch_kernel(side_front_kernel, attr[0], b, grid(0, SIDE_HOT_BLOCKS), WAVE, lds, s);
     b.hot_list = nullptr;
+    if (!rc && a.d.n_rp > 1)
+        rc = launch_kernel(cell_kernel, attr[7], b, grid(1, SIDE_MID_BLOCKS), NT_CELL, (size_t)cell_lds_bytes(H), s);
     if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_MID, NW_MID>, attr[6], b,
                                 grid(1, SIDE_MID_BLOCKS), NW_MID * WAVE,
                                 (size_t)mid_layout(H, a.d.sub_steps).bytes, s);

@@ -136,6 +136,8 @@ class MPCBatch:
         self.home_stride = int(home_stride)
         self.set_environment(oat if oat is not None else [0.0], ghi if ghi is not None else [0.0],
                              tou if tou is not None else [0.0], start_index)
+        self.workspace = None
+        self.lag = None
         self.set_reward_price(reward_price)
         self.vals = torch.full((L.NVAL, self.N), float("nan"), dtype=torch.float64, device=dev)
         # the forecast fields <key>_<j>: stored home-contiguous ([N][NFC][H], dragg_mi355x.h: one home's
@@ -154,11 +156,7 @@ class MPCBatch:
         if rc < 0:
             L.check(rc)
         self.lds_bytes = rc
-        ws = self.lib.dragg_mpc_workspace_bytes(ctypes.byref(self.dims))
-        if ws < 0:
-            L.check(int(ws))
-        self.workspace = torch.empty(max(1, (ws + 7) // 8), dtype=torch.int64, device=dev) if ws > 0 else None
-        self.lag = None
+        self._ensure_workspace()
 
     # ------------------------------------------------------------------ environment
     def set_environment(self, oat, ghi, tou, start_index):
@@ -184,6 +182,22 @@ class MPCBatch:
                              f"entries, horizon is {self.H}")
         self.rp = rp if torch.is_tensor(rp) else torch.tensor(rp, dtype=torch.float64, device=self.device)
         self.dims.n_rp = n
+        if self.workspace is not None or hasattr(self, "vals"):
+            self._ensure_workspace()
+
+    def _ensure_workspace(self):
+        """Device scratch of dragg_mpc_workspace_bytes(dims) bytes (it grows when a reward-price list makes
+        RL prices possible: the cell bound's rows); the lag mode's side workspace likewise."""
+        ws = self.lib.dragg_mpc_workspace_bytes(ctypes.byref(self.dims))
+        if ws < 0:
+            L.check(int(ws))
+        need = max(1, (ws + 7) // 8) if ws > 0 else 0
+        have = self.workspace.numel() if self.workspace is not None else 0
+        if need > have:
+            self.drain()
+            self.workspace = torch.empty(need, dtype=torch.int64, device=self.device)
+            if self.lag is not None:
+                self.lag["side_ws"] = torch.empty_like(self.workspace)
 
     # ------------------------------------------------------------------ structs
     def _problem(self):

@@ -25,6 +25,8 @@ homes = synthetic_homes(a.homes, seed=12, days=days, dt=dt, horizon_hours=hh)
 oat, ghi, tou = synthetic_weather(days, dt, math.ceil(a.steps / dt), seed=3, month=7)
 agg = DeviceAggregator(homes, oat, ghi, tou, 0, a.steps, reward_price=[0.0], seed=12, keep_history=False)
 H = agg.batch.H
+agg.batch.enable_phase_timing()
+ph_sum, ph_n = np.zeros(L.NPHASE), 0
 rng = np.random.default_rng(5)
 cnt = collections.Counter()
 for t in range(a.steps):
@@ -42,6 +44,14 @@ for t in range(a.steps):
         for v, n in zip(*np.unique(r[on == 1], return_counts=True)):
             cnt[(c, int(v))] += int(n)
     cnt["steps_dp"] += int(((p & L.PATH_STEPS) != 0).sum())
+    cyc = agg.batch.cycles.cpu().numpy().astype(float)
+    ph_sum += cyc.sum(1)
+    ph_n += cyc.shape[1]
     cnt["second"] += int(((p & L.PATH_SECOND) != 0).sum())
+    approx = (p & 1) != 0
+    for b, name in ((16, "cells"), (17, "beam_ub"), (18, "big")):
+        cnt[name] += int(((p >> b) & 1).sum())
+        cnt[name + "_approx"] += int((((p >> b) & 1) & approx).sum())
     print(f"t={t}: {e0.elapsed_time(e1):.1f} ms, statuses {np.bincount(st).tolist()}", flush=True)
 print({str(k): v for k, v in cnt.items()})
+print("mean shader cycles per home-step by phase:", {n: round(v / max(1, ph_n)) for n, v in zip(L.PHASES, ph_sum)})
