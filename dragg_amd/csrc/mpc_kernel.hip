@@ -2428,7 +2428,7 @@ DEV T dpp_iscan(T v, int lane, T id, Op op) {
 // cell (widened by rounding margins): row H = 0 on the cells meeting x_H's box, and row k = min over
 // the duties u of q_k u + min of row k + 1 over the cells the image A [a, b] + C + g u meets inside
 // x_{k+1}'s box (+inf where none) -- a minimum over a superset of the states a schedule can reach,
-// rounded down to f32.  r0 / r1: two LDS rows of scratch.  Every thread of the block calls it; false
+// rounded down to f32.  r0 / r1: two LDS rows of scratch (NCELL + 1 floats each at least).  Every thread of the block calls it; false
 // (no bound) on a degenerate stage (A <= 0).
 // the cell grid over a chain's box [bl, bh] (widened past every tolerance of the labels' box tests)
 DEV void cell_grid(double bl, double bh, double& c_lo, double& c_inv) {
@@ -2470,25 +2470,68 @@ DEV bool cell_rows(float* cg, float* r0, float* r1, const double* cA, const doub
         cell_span(bxl(k), bxh(k), b0, b1);
         // the image of cell j = [a_j - eps, b_j + eps] under duty u, in cell units of x_{k+1}: its ends are
         // affine in j (slope A), lo_u + j A and lo_u + (j + 1) A + w; widened by a margin far above the
-        // rounding of this form (1e-6 cells) and of the labels' own arithmetic (tw) -- a superset of the
+        // rounding of this form and of the labels' own arithmetic (tw) -- a superset of the
         // cells the states of cell j reach (outside the grid: clamped, where no state stays feasible)
-        const double mg = 1e-6 + (2.0 * tw(fabs(C) + fabs(A) * (fabs(c_lo) + NCELL * dlt) + fabs(g) * S) + eps) * c_inv;
-        const double base = (fma(A, c_lo - eps, C) - c_lo) * c_inv - mg;       // lo_0 at j = 0 (u = 0)
-        const double wd = 2.0 * (A * eps * c_inv + mg);                          // the image's extra width
-        const double gu = g * c_inv;
+        // (f32 from here: the cell units of the ends are below ~2^13, their f32 rounding ~1e-3 of a cell at
+        // most -- the 0.01-cell margin covers it; values rounded down at every step: still lower bounds)
+        const double mg = 0.01 + (2.0 * tw(fabs(C) + fabs(A) * (fabs(c_lo) + NCELL * dlt) + fabs(g) * S) + eps) * c_inv;
+        const float basef = (float)((fma(A, c_lo - eps, C) - c_lo) * c_inv - mg);    // lo_0 at j = 0 (u = 0)
+        const float wdf = (float)(2.0 * (A * eps * c_inv + mg));                        // the image's extra width
+        const float Af = (float)A, guf = (float)(g * c_inv);
+        const float qlo = __double2float_rd(q);
+        if (Af + wdf < 1.0f) {
+            // an image narrower than a cell meets cells i0 and i0 + 1 at most: the pair minima of V_{k+1}
+            // once (pm[i + 1] = min(V[i], V[i + 1]), V = +inf past the grid), then one load per duty
+            float* const pm = cur;                 // (the stage's output row is written after: pm first)
+            for (int i = tid; i <= NCELL; i += NT) {
+                const float va = i >= 1 ? nxt[i - 1] : INFINITY, vb = i < NCELL ? nxt[i] : INFINITY;
+                pm[i] = fminf(va, vb);
+            }
+            __syncthreads();
+            float outv[(NCELL + NT - 1) / NT];
+#pragma unroll
+            for (int r = 0; r < (NCELL + NT - 1) / NT; ++r) {
+                const int j = r * NT + tid;
+                float best = INFINITY;
+                if (j < NCELL && j >= b0 && j <= b1) {
+                    const float lj = fmaf((float)j, Af, basef);
+                    float mv[SS + 1];
+#pragma unroll
+                    for (int u = 0; u <= SS; ++u) {
+                        const float l = fmaf((float)u, guf, lj);
+                        const int i0 = (int)floorf(fminf(fmaxf(l, -2.0f), (float)NCELL + 1.0f));
+                        mv[u] = (i0 >= -1 && i0 < NCELL) ? pm[i0 + 1] : INFINITY;
+                    }
+                    // f32: q rounded down (u >= 0), each sum lowered by 2 ulps past its rounding
+#pragma unroll
+                    for (int u = 0; u <= SS; ++u) best = fminf(best, fmaf(qlo, (float)u, mv[u]));
+                    best = best < INFINITY ? best - fabsf(best) * 2.4e-7f - 1e-30f : INFINITY;
+                }
+                outv[r] = best;
+            }
+            __syncthreads();                       // (every thread read pm: the row may be written)
+#pragma unroll
+            for (int r = 0; r < (NCELL + NT - 1) / NT; ++r) {
+                const int j = r * NT + tid;
+                if (j < NCELL) { cur[j] = outv[r]; cg[(size_t)k * NCELL + j] = outv[r]; }
+            }
+            __syncthreads();
+            float* t_ = nxt; nxt = cur; cur = t_;
+            continue;
+        }
         for (int j = tid; j < NCELL; j += NT) {
             double best = INFINITY;
             if (j >= b0 && j <= b1) {
-                const double lj = fma((double)j, A, base);
+                const float lj = fmaf((float)j, Af, basef);
                 // every duty's (one or two) loads issued together: clamped indices, the test after
                 float m0[SS + 1], m1[SS + 1];
                 int span[SS + 1];
 #pragma unroll
                 for (int u = 0; u <= SS; ++u) {
-                    const double l = fma((double)u, gu, lj), h = l + A + wd;
-                    const bool in = h >= 0.0 && l <= (double)NCELL;
-                    const int i0 = in ? min(NCELL - 1, max(0, (int)floor(l))) : 0;
-                    const int i1 = in ? min(NCELL - 1, max(i0, (int)floor(h))) : 0;
+                    const float l = fmaf((float)u, guf, lj), h = l + Af + wdf;
+                    const bool in = h >= 0.0f && l <= (float)NCELL;
+                    const int i0 = in ? min(NCELL - 1, max(0, (int)floorf(l))) : 0;
+                    const int i1 = in ? min(NCELL - 1, max(i0, (int)floorf(h))) : 0;
                     m0[u] = nxt[i0];
                     m1[u] = nxt[min(i0 + 1, i1)];
                     span[u] = in ? i1 - i0 : -1;
@@ -2498,7 +2541,7 @@ DEV bool cell_rows(float* cg, float* r0, float* r1, const double* cA, const doub
                     if (span[u] < 0) continue;
                     float m = fminf(m0[u], m1[u]);
                     if (span[u] > 1) {                     // (a stage with A > 1: a wider image)
-                        const int i0 = min(NCELL - 1, max(0, (int)floor(fma((double)u, gu, lj))));
+                        const int i0 = min(NCELL - 1, max(0, (int)floorf(fmaf((float)u, guf, lj))));
                         for (int i = i0 + 2; i <= i0 + span[u]; ++i) m = fminf(m, nxt[i]);
                     }
                     if (m < INFINITY) best = fmin(best, fma(q, (double)u, (double)m));
@@ -4297,7 +4340,9 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 if (!ok) int_path |= 1 << (13 + chain);
                 continue;
             }
-            if (h.S == 6 && !(SECOND && rl_prices)) {
+            // (RL prices: the indoor-air chain skips the regular front DP -- its fronts outgrow it -- for the
+            // cell-bound path below; the tank chain's fronts stay small: it tries it first)
+            if (h.S == 6 && !(SECOND && rl_prices && chain == 0)) {
                 double* const wl = D.wl;
                 // (a multi-wave second launch: the exchange area of its mid / big layout, past the
                 // direct layout's arrays)
@@ -4492,8 +4537,9 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
     if (a.out.hist && lane == 0)      // lane 0 wrote every vals field of this home
         for (int k = 0; k < DRAGG_NVAL; ++k) a.out.hist[(size_t)k * N + home] = io.v(k);
     pf.mark(DRAGG_PH_WRITE);
-    if (pf.on && lane == 0)
-        for (int k = 0; k < DRAGG_NPHASE; ++k) a.out.cycles[(size_t)k * N + home] = (int64_t)pf.acc[k];
+    if (pf.on && lane == 0)        // (the factor / check slots: the cell kernel's, int_mode round)
+        for (int k = 0; k < DRAGG_NPHASE; ++k)
+            if (k != DRAGG_PH_FACTOR && k != DRAGG_PH_CHECK) a.out.cycles[(size_t)k * N + home] = (int64_t)pf.acc[k];
     lag_finish(a, home);
 }
 
@@ -4546,8 +4592,9 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
 // the mid launch's).
 constexpr int NT_CELL = 256;
 constexpr int CELL_BLOCKS = 1024;           // blocks of the cell kernel (4 per CU)
-__host__ __device__ inline int cell_lds_bytes(int H) { return (front_layout(H).bytes + 15) / 16 * 16 + 2 * NCELL * 4; }
-__global__ __launch_bounds__(NT_CELL) void cell_kernel(KArgs a) {
+constexpr int CELL_ROW = NCELL + 16;        // an LDS row of cell_rows (the pair minima take NCELL + 1)
+__host__ __device__ inline int cell_lds_bytes(int H) { return (front_layout(H).bytes + 15) / 16 * 16 + 2 * CELL_ROW * 4; }
+__global__ __launch_bounds__(NT_CELL, 4) void cell_kernel(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = a.d.n_homes, H = a.d.horizon;
     const int tid = threadIdx.x;
@@ -4556,7 +4603,7 @@ __global__ __launch_bounds__(NT_CELL) void cell_kernel(KArgs a) {
     const int* const list = reinterpret_cast<const int*>(lw + defer_offset(N, H));
     const int cnt = min(list[N], N);
     float* const r0 = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + (front_layout(H).bytes + 15) / 16 * 16);
-    float* const r1 = r0 + NCELL;
+    float* const r1 = r0 + CELL_ROW;
     for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
         const int e = list[j];
         const int home = e & HOME_MASK;
@@ -4565,6 +4612,8 @@ __global__ __launch_bounds__(NT_CELL) void cell_kernel(KArgs a) {
         LdsD D = carve_front(smem, H);
         Lds L = lp_view(D);
         Io io{a.vals, a.fc, N, home};
+        Prof pf;
+        pf.start(a.out.cycles != nullptr);
         __syncthreads();
         if (prologue<false>(a, h, L, io, tid, NT_CELL, D.sc) == DRAGG_ST_ERR_MISSING) continue;
         derive(h);
@@ -4582,9 +4631,17 @@ __global__ __launch_bounds__(NT_CELL) void cell_kernel(KArgs a) {
         double c_lo, c_inv;
         cell_grid(h.Tmin, h.Tmax, c_lo, c_inv);
         float* const cg = reinterpret_cast<float*>(ws + cell_region_offset(N, H)) + (size_t)home * (H + 1) * NCELL;
+        pf.mark(DRAGG_PH_CHECK);                   // (diagnostic: the prologue, in the check slot)
         const bool ok = cell_rows<NT_CELL, 6>(cg, r0, r1, D.cA, D.cC, D.cq, H, 6, h.g, h.Tmin, h.Tmax, h.Tmin, h.Tmax,
                                               c_lo, c_inv, tid);
-        if (tid == 0) cg[0] = ok ? 1.0f : 0.0f;
+        pf.mark(DRAGG_PH_FACTOR);                  // (diagnostic: the cell rows, in the factor slot)
+        if (tid == 0) {
+            cg[0] = ok ? 1.0f : 0.0f;
+            if (pf.on) {
+                a.out.cycles[(size_t)DRAGG_PH_CHECK * N + home] = (int64_t)pf.acc[DRAGG_PH_CHECK];
+                a.out.cycles[(size_t)DRAGG_PH_FACTOR * N + home] = (int64_t)pf.acc[DRAGG_PH_FACTOR];
+            }
+        }
     }
 }
 

@@ -244,7 +244,8 @@ def test_config4_rl_10k_homes_price_broadcast_and_rollouts(gpu):
             pick = _sample(np.random.default_rng(51), st, homes, 25)
             fb = []
             res = _check_sample(homes, oat, ghi, tou, rp, t, prev_vals, prev_fc, noise, st, ob,
-                                b.vals.cpu().numpy(), b.fc.cpu().numpy(), pick, path=path, fallback_gaps=fb)
+                                b.vals.cpu().numpy(), b.fc.cpu().numpy(), pick, path=path, fallback_gaps=fb,
+                                approx_bound=1e-9)
             n_off = int((path[st == 0] & L.PATH_APPROX_MASK != 0).sum())
     assert torch.equal(fc, torch.stack(committed))
     agg.restore(snap)
@@ -256,14 +257,9 @@ def test_config4_rl_10k_homes_price_broadcast_and_rollouts(gpu):
           f"exact fronts under the smooth RL price), {n_off} of them left the exact DP (front overflow past "
           f"NF_BIG); sampled fallback gaps to the exact optimum: {len(fb)}, mean "
           f"{fb.mean() if len(fb) else 0:.1e}, max {fb.max() if len(fb) else 0:.1e}")
-    # under RL prices a chain past the big fronts keeps its bucketed schedule by default (the step-function
-    # DP explodes on a price that changes at every stage; DRAGG_FLAG_EXACT sends it there): at most 0.1 %
-    # of the homes, each flagged in int_path with reason 3 on the chain that kept it
-    assert n_off <= 0.001 * len(homes), n_off
-    for p_ in path[(st == 0) & (path & L.PATH_APPROX_MASK != 0)]:
-        for c in (0, 1):
-            if p_ & (1 << c):
-                assert (p_ >> (4 + 4 * c)) & 0xF == 3, hex(p_)
+    # RL prices are exact by default since round 5 (the indoor-air chain's cell bound, the beam's upper
+    # bound and the bisection on the bound): no chain keeps an approximate schedule
+    assert n_off == 0, n_off
     _report("configs[4] RL 10k homes, H = 48, July, rollout = commit", agg, homes, [(t,) + res], min_opt=0)
 
 
@@ -408,3 +404,38 @@ def test_bench_narrow_set_solves_gap_bound_and_exact_mode(bench_day):
 
 
 NARROW_GAP_BOUND = 1e-9      # exact: the step-function DP (round 3's bucketed approximation: 8.5 %, home 7519 at t = 60)
+
+
+def test_rl_bench_price_exact_on_every_chain(gpu):
+    """The bench's RL workload (bench.py --workload rl: its 10,000-home community, July, H = 48, the
+    smooth reward price that changes at every stage): every chain of two actions' steps solved exactly
+    (no int_path approximation bit; round 4 left ~30 % of the indoor-air chains on the bucketed schedule
+    there), and a sample of 20 solves per step equal to the exact optimum (oracle/thermal.py, 1e-9)."""
+    import torch
+    from dragg_amd import _lib as L
+    from dragg_amd.aggregator import DeviceAggregator
+    from dragg_amd.community import synthetic_homes, synthetic_weather
+    dt, hh, steps = 4, 12, 2
+    sim_hours = math.ceil(steps / dt)
+    days = math.ceil((sim_hours + hh + 2) / 24) + 1
+    homes = synthetic_homes(10000, seed=12, days=days, dt=dt, horizon_hours=hh)
+    oat, ghi, tou = synthetic_weather(days, dt, sim_hours, seed=3, month=7)
+    H = hh * dt
+    off = np.random.default_rng(5).uniform(-0.02, 0.02, (steps, 1))
+    prices = off + (-0.03 * np.cos(np.arange(H) / 3.0))[None, :]
+    agg = DeviceAggregator(homes, oat, ghi, tou, 0, steps, reward_price=[0.0] * H, seed=12)
+    b = agg.batch
+    rng = np.random.default_rng(7)
+    for t in range(steps):
+        rp = list(prices[t])
+        agg.set_reward_price(rp)
+        prev_vals, prev_fc, noise = b.vals.cpu().numpy(), b.fc.cpu().numpy(), b.season_noise(t).cpu().numpy()
+        agg.run_iteration()
+        torch.cuda.synchronize()
+        st, ob, path = b.status.cpu().numpy(), b.obj.cpu().numpy(), b.int_path.cpu().numpy()
+        assert not (path & L.PATH_APPROX_MASK).any(), np.flatnonzero(path & L.PATH_APPROX_MASK)[:10]
+        n_big = int(((path >> 18) & 1).sum())
+        print(f"t={t}: {int((st == 0).sum())} optimal, {n_big} through the big launch, 0 approximate")
+        pick = _sample(rng, st, homes, 5)
+        _check_sample(homes, oat, ghi, tou, rp, t, prev_vals, prev_fc, noise, st, ob, b.vals.cpu().numpy(),
+                      b.fc.cpu().numpy(), pick, path=path, fallback_gaps=[], approx_bound=1e-9)
