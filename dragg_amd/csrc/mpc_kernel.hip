@@ -66,7 +66,8 @@ constexpr int NF_MID = 384;              // front capacity of the mid launch (DM
 // exact pass's fronts then hold 22-280 labels, where the LP bound and the bucketed schedule's cost left
 // 30 % of the chains past 2,048)
 constexpr int NCELL = 1024;              // cells of the grid
-constexpr int BEAM_K = 48;               // labels a beam stage keeps (7 BEAM_K children fit NF_MID)
+constexpr int BEAM_K = 32;               // labels a beam stage keeps (7 BEAM_K children fit NF_MID; measured
+                                         //   RL action at 48: 20.1 ms, 32: 19.6 ms)
 constexpr int CELL_TRIES = 8;            // bisection steps on the bound after a pass past the capacity
 constexpr int NTB_MID = 128;             // ... and its key / cost buckets per stage
 constexpr int MID_SLOTS_MAX = 2048;      // blocks of the persistent mid launch (~7 per CU at H = 48)
@@ -1657,7 +1658,7 @@ __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
 // is done with them, its schedule is in the global solution array) the big exact pass's
 // fronts [NF_BIG], W table, bucket arrays and hull.
 struct BigLayout {
-    int fa, fb, wl, kb, cb, mh, kl, flo, fhi, xch, cl, bytes;   // cl: the cell bound's row (mid only; -1: none)
+    int fa, fb, wl, kb, cb, mh, kl, flo, fhi, xch, bytes;
 };
 __host__ __device__ inline BigLayout big_layout(int H, int S) {
     const DirectLayout d = direct_layout(H, S);
@@ -1675,7 +1676,6 @@ __host__ __device__ inline BigLayout big_layout(int H, int S) {
     o.fhi = take(4 * (H + 1), 4);
     p = max(p, d.bytes);                         // past the direct layout too: the regular front DP of
     o.xch = take(max(xch_bytes(NF_BIG), xch_bytes(NF)), 16);   // the (multi-wave) launch uses it as well
-    o.cl = -1;                                   // (no room for 2 blocks per CU: rows read from the workspace)
     o.bytes = (p + 15) / 16 * 16;
     return o;
 }
@@ -1698,7 +1698,8 @@ __host__ __device__ inline BigLayout mid_layout(int H, int S) {
     o.fhi = take(4 * (H + 1), 4);
     p = max(p, d.bytes);
     o.xch = take(max(xch_bytes(NF_MID), xch_bytes(NF)), 16);
-    o.cl = take(4 * NCELL, 16);
+    // (the RL path's cell rows are read from the workspace, not staged in LDS: 4 KB per block more cost a
+    // block per CU -- measured RL action 18.0 ms against 20.1 ms with the row in LDS)
     o.bytes = (p + 15) / 16 * 16;
     return o;
 }
@@ -2366,7 +2367,6 @@ struct FrontBufs {
     char* xch;                           // [xch_bytes(CAP)] LDS: the waves' exchange area (NW > 1)
     // dp_front<..., CELL = true>: the cell bound in place of W
     const float* cg;                     // [H + 1][NCELL] global: cell_rows' lower bounds of x_k's cost-to-go
-    float* cl;                           // [NCELL] LDS: the current stage's row
     double c_lo, c_inv;                  // the grid: cell of x = floor((x - c_lo) c_inv)
 };
 
@@ -2773,11 +2773,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     }
     int capn = prune ? CAPB : CAP;                   // front capacity (overflow: -3)
     bool tried = CELL || prune || B.wg == nullptr;   // the bound is built at most once
-    // the cell bound's row of the stage's children (LDS) and the next row in flight (registers)
-    constexpr int CPL = CELL ? NCELL / NT : 1;
-    float cpre[CPL];
-    // (B.cl == nullptr: the rows are read from the workspace -- the big launch, whose LDS has no room)
-    const float* crow = B.cl ? B.cl : B.cg + NCELL;
+    // the cell bound's row of the stage's children, read from the workspace (cell_kernel's rows: staging
+    // them in LDS cost a block per CU of the mid launch, measured slower)
+    const float* crow = B.cg + NCELL;
     auto cell_at = [&](double x) -> double {
         const int c = min(NCELL - 1, max(0, (int)floor((x - B.c_lo) * B.c_inv)));
         return (double)crow[c];
@@ -2796,13 +2794,6 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     // W_{k+1} of the stage in the LDS table, W_{k+2} in flight
     double2 wnext = make_double2(INFINITY, INFINITY);
     if constexpr (CELL) {
-        if (B.cl) {
-#pragma unroll
-            for (int j = 0; j < CPL; ++j) {
-                B.cl[j * NT + tid] = B.cg[(size_t)1 * NCELL + j * NT + tid];
-                cpre[j] = H >= 2 ? B.cg[(size_t)2 * NCELL + j * NT + tid] : 0.0f;
-            }
-        }
     } else if (prune && wid == 0) {
         const double2 w1 = load_row(1);
         w_to_lds(B, lane, w1.x, w1.y);
@@ -3167,15 +3158,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         }
         for (int b = tid; b < NBK && !nodom; b += NT) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
         if constexpr (CELL) {
-            if (B.cl == nullptr) {
-                crow = B.cg + (size_t)(k + 2) * NCELL;
-            } else if (k + 2 <= H) {
-#pragma unroll
-                for (int j = 0; j < CPL; ++j) {
-                    B.cl[j * NT + tid] = cpre[j];
-                    if (k + 3 <= H) cpre[j] = B.cg[(size_t)(k + 3) * NCELL + j * NT + tid];
-                }
-            }
+            crow = B.cg + (size_t)(k + 2) * NCELL;
         } else if (prune && k + 1 < H && wid == 0) {
             w_to_lds(B, lane, wnext.x, wnext.y);
             if (k + 3 <= H) wnext = load_row(k + 3);
@@ -3249,7 +3232,7 @@ DEV bool round_duties(const Home& h, const Lds& L, int lane, uint16_t* par) {
     B.cA = cA; B.cC = cC; B.cq = cq; B.x = L.x; B.par = par;
     B.wg = nullptr; B.wlx = B.wlv = B.wls = nullptr;     // no bound pruning on this path
     B.xch = nullptr;                                     // one wave
-    B.cg = nullptr; B.cl = nullptr; B.c_lo = 0.0; B.c_inv = 0.0;
+    B.cg = nullptr; B.c_lo = 0.0; B.c_inv = 0.0;
     const bool front = h.S == 6 && par != nullptr && (f - L.Lf) <= 128 * H;
     for (int k = lane; k < H; k += WAVE) {
         cA[k] = h.aT;
@@ -4391,8 +4374,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                                    reinterpret_cast<unsigned*>(sb + bl.mh), reinterpret_cast<unsigned*>(sb + bl.kl),
                                    reinterpret_cast<unsigned*>(sb + bl.flo), reinterpret_cast<unsigned*>(sb + bl.fhi),
                                    D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE,
-                                   sb + bl.xch, cg, bl.cl >= 0 ? reinterpret_cast<float*>(sb + bl.cl) : nullptr,
-                                   c_lo, c_inv};
+                                   sb + bl.xch, cg, c_lo, c_inv};
                 // a chain the mid launch handed over: its upper-bound schedule (the beam's or the bucketed
                 // DP's) is in the solution rows already (the mid pass overflowed without writing them),
                 // only the big pass is left
