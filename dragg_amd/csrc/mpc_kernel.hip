@@ -3060,12 +3060,18 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             // bucket), the threshold by two histogram levels; in-order compaction chunk by chunk (a label
             // only moves down), its back-pointer with it
             if (beam_k > 0 && nn > beam_k && nn <= capn) {
+                // each label's cost + bound once (its cell row is in the workspace) into the key buckets'
+                // LDS, free until the stage's end (beam fronts: nn <= 7 beam_k <= NBK doubles)
+                double* const fv = reinterpret_cast<double*>(B.kb);
+                const bool fcache = nn <= NBK;
                 double fl = INFINITY, fh = -INFINITY;
                 for (int i = lane; i < nn; i += WAVE) {
                     const double2 Li = fb[i];
                     const double f = Li.y + cell_at(Li.x);
+                    if (fcache) fv[i] = f;
                     fl = fmin(fl, f); fh = fmax(fh, f);
                 }
+                auto f_of = [&](int i) { return fcache ? fv[i] : fb[i].y + cell_at(fb[i].x); };
                 fl = dpp_reduce(fl, [](double a_, double b_) { return fmin(a_, b_); });
                 fh = dpp_reduce(fh, [](double a_, double b_) { return fmax(a_, b_); });
                 // the threshold by two histograms of 64 buckets (LDS atomics): over [fl, fh], then over the
@@ -3083,7 +3089,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     hl[lane] = 0;
                     wave_sync();
                     for (int i = lane; i < nn; i += WAVE) {
-                        const double f = fb[i].y + cell_at(fb[i].x);
+                        const double f = f_of(i);
                         if (f >= thr_lo && (lvl == 0 || f < bl_ + 64.0 / bsc)) {
                             const int bk = bucket_of(f, bl_, bsc);
                             if (bk < 64) atomicAdd(hl + bk, 1);
@@ -3119,7 +3125,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     if (i < nn) {
                         Li = fb[i];
                         pr = B.par[k * PS + i];
-                        const double f = Li.y + cell_at(Li.x);
+                        const double f = f_of(i);
                         must = f < thr_in;
                         cand = !must && f < fcut;
                     }
