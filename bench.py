@@ -59,6 +59,9 @@ def parse(argv=None):
                          "with --homes 20 --cpu-home-steps 1920)")
     ap.add_argument("--cpu-milp-limit", type=float, default=300.0,
                     help="HiGHS time limit per CPU solve; solves that reach it are counted separately")
+    ap.add_argument("--cpu-home-range", default=None,
+                    help="CPU baseline: only the sampled homes [a:b) of the sample (a workload split by home over "
+                         "several runs, e.g. configs[0] in full over two GPU-box calls; tools/merge_cpu_parts.py)")
     ap.add_argument("--cpu-only", action="store_true",
                     help="run only the CPU baseline (no GPU) and print its JSON (the committed full run)")
     ap.add_argument("--workload", default="rbo", choices=["rbo", "rl"],
@@ -162,7 +165,7 @@ def _cpu_worker(args):
     return n, times, limited[0]
 
 
-def cpu_baseline(homes, env, seconds, workers, home_steps, milp_limit=300.0, steps_per_home=4):
+def cpu_baseline(homes, env, seconds, workers, home_steps, milp_limit=300.0, steps_per_home=4, home_range=None):
     """The reference's per-home solve restated on the host (oracle/mpc.py: the reference's problem
     build, HiGHS MILP standing in for GLPK_MI, cleanup/fallback), one process per host core this
     job may use (one process per core), on `home_steps` home-steps of this workload
@@ -176,6 +179,11 @@ def cpu_baseline(homes, env, seconds, workers, home_steps, milp_limit=300.0, ste
     deadline = time.time() + seconds if seconds > 0 else 0.0
     n_homes = max(workers, -(-home_steps // steps_per_home))
     picks = [homes[(i * 7919) % len(homes)] for i in range(n_homes)]
+    if home_range:
+        a_, b_ = (int(x) for x in home_range.split(":"))
+        picks = picks[a_:b_]
+        home_steps = min(home_steps, len(picks) * steps_per_home)
+        workers = min(workers, len(picks))
     per = [picks[w::workers] for w in range(workers)]
     # a sample covering every step of every home (configs[0] in full) runs each home's whole loop
     quota = -(-home_steps // workers) if n_homes * steps_per_home > home_steps else 1 << 40
@@ -190,6 +198,8 @@ def cpu_baseline(homes, env, seconds, workers, home_steps, milp_limit=300.0, ste
     # sample's wall budget (its incumbent kept) is excluded from the count but its time is not
     done = n - limited
     return {"value": done / wall if wall > 0 else 0.0, "unit": "solves/s", "cores": workers, "host_cores": info,
+            "home_range": home_range, "solve_cpu_s": float(np.sum(times)) if times else 0.0,
+            "done_home_steps": done,
             "value_incl_cut_solves": n / wall if wall > 0 else 0.0,
             "kind": "port", "home_steps": n, "target_home_steps": home_steps, "time_limited_solves": limited,
             "extrapolated": True, "wall_s": wall,
@@ -459,7 +469,7 @@ def main():
            "rp_steps": [list(map(float, prices[t])) for t in range(args.cpu_steps_per_home)] if rl else None}
     cpu_args = (args.cpu_seconds, args.cpu_workers, args.cpu_home_steps, args.cpu_milp_limit, args.cpu_steps_per_home)
     if args.cpu_only:
-        out = cpu_baseline(homes, env, *cpu_args)
+        out = cpu_baseline(homes, env, *cpu_args, home_range=args.cpu_home_range)
         out["workload"] = cpu_workload_key(n_total, Hh, dt, args.month, args.rl_price if rl else None)
         print(json.dumps(out))
         return
