@@ -18,6 +18,8 @@ fi
 args_of() {
   case $1 in
     driver) echo --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 ;;
+    drivers) echo --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --no-overlap ;;
+    shard8m7) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 --shard-rank 7 ;;
     full96) echo --steps 96 --warmup 4 --cpu-seconds 0 ;;
     full96s) echo --steps 96 --warmup 4 --cpu-seconds 0 --no-overlap ;;
     shard8maxs) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 --shard-max --no-overlap ;;
