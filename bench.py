@@ -649,7 +649,7 @@ def main():
                                       "side stream's step-function DP runs beside it and is in the wall time)"},
             "cpu_baseline": (headline_cpu_baseline(committed_cpu_baseline(cpu_workload_key(n_total, Hh, dt, args.month,
                                                                                             args.rl_price if rl else None)), cpu)
-                             if (rank == 0 and world == 1) else None),
+                             if rank == 0 else None),       # (world > 1: the committed run only)
             "status_counts": stat_counts,
             # RL: the headline counts the rollout re-solves too; the committed steps alone:
             "committed_solves_per_s": n_total * args.steps / elapsed,

@@ -20,6 +20,7 @@ args_of() {
     driver) echo --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 ;;
     drivers) echo --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --no-overlap ;;
     shard8m7) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 --shard-rank 7 ;;
+    shard8m7s) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 --shard-rank 7 --no-overlap ;;
     full96) echo --steps 96 --warmup 4 --cpu-seconds 0 ;;
     full96s) echo --steps 96 --warmup 4 --cpu-seconds 0 --no-overlap ;;
     shard8maxs) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 --shard-max --no-overlap ;;
@@ -41,9 +42,9 @@ run() { name=$1
   grep '^{' $OUT/$name.out | tail -1 > $OUT/$name.json
   python3 -c "
 import json; d=json.load(open('$OUT/$name.json')); print('$name', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],4), 'ms/step', 'kern', round(d['roofline']['kernel_ms'],4), (d.get('shard_emulation') or {}).get('max_over_shards'), {k: v for k, v in d['status_counts'].items() if v and k != 'optimal'})"; }
-for spec in ${LINES:-full96}; do run $spec; done
-if [ -n "$TRACE" ]; then
-  timeout -k 10 ${LINE_LIMIT:-400} rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$TRACE -o run -- python3 bench.py $(args_of $TRACE) > $OUT/trace_$TRACE.log 2>&1 || { echo "trace failed"; tail -5 $OUT/trace_$TRACE.log; exit 1; }
-  f=$(find $OUT/trace_$TRACE -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && head -8 "$f"
-fi
+for spec in ${LINES:-full96}; do [ "$spec" = none ] || run $spec; done
+for TR in $TRACE; do
+  timeout -k 10 ${LINE_LIMIT:-400} rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$TR -o run -- python3 bench.py $(args_of $TR) > $OUT/trace_$TR.log 2>&1 || { echo "trace failed"; tail -5 $OUT/trace_$TR.log; exit 1; }
+  f=$(find $OUT/trace_$TR -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && head -8 "$f"
+done
 echo session-done
