@@ -29,10 +29,15 @@ def _hot(name):
     return re.search(r"mpc_direct_kernel<false, 0[,>]", name) is not None or "mpc_home_kernel<false>" in name
 
 
-def step_groups(rows, n_units, per_unit, kernel_sub="mpc_"):
+def _ours(name):
+    """the solver's launches: mpc_* kernels, the RL cell bound (cell_kernel), the lag mode's side hot launch"""
+    return "mpc_" in name or "cell_kernel" in name or "side_front_kernel" in name
+
+
+def step_groups(rows, n_units, per_unit):
     """rows: (dispatch_id, kernel_name, payload) of one pass.  -> the last n_units units, each a list
     of payloads (a unit = per_unit consecutive step groups)."""
-    rows = sorted((r for r in rows if kernel_sub in r[1]), key=lambda r: r[0])
+    rows = sorted((r for r in rows if _ours(r[1])), key=lambda r: r[0])
     groups = []
     for d, name, pay in rows:
         if _hot(name) or not groups:
@@ -46,13 +51,21 @@ def step_groups(rows, n_units, per_unit, kernel_sub="mpc_"):
 
 
 def trace_ms(path, n_units, per_unit):
-    rows = []
-    for r in csv.DictReader(open(path)):
-        rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"],
-                     (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6))
-    units = step_groups(rows, n_units, per_unit)
+    """(mean, per-unit) kernel ms of the launches on the hot launch's stream, and the mean per unit of
+    those on other streams (lag mode's side pass: it runs beside the main pass, so it is reported apart
+    and not added; bench.py's HIP events time the main stream)"""
+    rows = list(csv.DictReader(open(path)))
+    hot_streams = {r.get("Stream_Id") for r in rows if _hot(r["Kernel_Name"])}
+    main, side = [], []
+    for r in rows:
+        t = (int(r["Dispatch_Id"]), r["Kernel_Name"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+        (main if r.get("Stream_Id") in hot_streams else side).append(t)
+    units = step_groups(main, n_units, per_unit)
     per = [sum(u) for u in units]
-    return sum(per) / len(per), per
+    side_ms = sum(t[2] for t in side if _ours(t[1])) / max(1, len(units))
+    if side and not any(_ours(t[1]) for t in side):
+        side_ms = 0.0
+    return sum(per) / len(per), per, side_ms
 
 
 def counters(path, n_units, per_unit):
@@ -95,9 +108,10 @@ def main():
     per_unit = 1 + fh
     key = traffic_key(a.homes, a.horizon, a.dt, a.month, a.int_mode, a.world, a.workload, a.steps, a.warmup,
                       a.rl_price if rl else None, fh)
-    ms, per = trace_ms(os.path.join(a.prof, "trace", "trace_kernel_trace.csv"), a.steps, per_unit)
+    ms, per, side_ms = trace_ms(os.path.join(a.prof, "trace", "trace_kernel_trace.csv"), a.steps, per_unit)
     out = {"workload": key, "command": a.command, "unit": "action" if rl else "step",
-           "kernel_ms_per_step": ms, "kernel_ms_per_step_min_max": [min(per), max(per)]}
+           "kernel_ms_per_step": ms, "kernel_ms_per_step_min_max": [min(per), max(per)],
+           "side_stream_kernel_ms_per_step": side_ms}
     f = counters(os.path.join(a.prof, "fetch", "fetch_counter_collection.csv"), a.steps, per_unit)["FETCH_SIZE"]
     w = counters(os.path.join(a.prof, "write", "write_counter_collection.csv"), a.steps, per_unit)["WRITE_SIZE"]
     out.update({"fetch_size_kb_per_step": f, "write_size_kb_per_step": w, "bytes_per_step": (2.0 * f + w) * 1024.0,
