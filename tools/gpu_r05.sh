@@ -28,6 +28,9 @@ args_of() {
     shard8) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 ;;
     shard8max) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 --shard-max ;;
     shard4max) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 4 --shard-max ;;
+    shard8maxd) echo --steps 20 --warmup 5 --cpu-seconds 0 --shard-of 8 --shard-max ;;
+    shard4maxd) echo --steps 20 --warmup 5 --cpu-seconds 0 --shard-of 4 --shard-max ;;
+    shard2maxd) echo --steps 20 --warmup 5 --cpu-seconds 0 --shard-of 2 --shard-max ;;
     shard2max) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 2 --shard-max ;;
     rl) echo --workload rl --steps 6 --warmup 1 --cpu-seconds 0 ;;
     cfg1) echo --homes 1000 --horizon-hours 6 --month 1 --steps 96 --warmup 4 --cpu-seconds 0 ;;

@@ -111,7 +111,8 @@ def main():
     ms, per, side_ms = trace_ms(os.path.join(a.prof, "trace", "trace_kernel_trace.csv"), a.steps, per_unit)
     out = {"workload": key, "command": a.command, "unit": "action" if rl else "step",
            "kernel_ms_per_step": ms, "kernel_ms_per_step_min_max": [min(per), max(per)],
-           "side_stream_kernel_ms_per_step": side_ms}
+           "side_stream_kernel_span_ms_per_step": side_ms,
+           "side_stream_note": "lag mode: summed start-to-end spans of the side pass launches, which run beside the main pass (a span includes the wait for dispatch slots), not added to kernel_ms_per_step"}
     f = counters(os.path.join(a.prof, "fetch", "fetch_counter_collection.csv"), a.steps, per_unit)["FETCH_SIZE"]
     w = counters(os.path.join(a.prof, "write", "write_counter_collection.csv"), a.steps, per_unit)["WRITE_SIZE"]
     out.update({"fetch_size_kb_per_step": f, "write_size_kb_per_step": w, "bytes_per_step": (2.0 * f + w) * 1024.0,
