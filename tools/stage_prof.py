@@ -22,13 +22,14 @@ ap.add_argument("--homes", type=int, default=10000)
 ap.add_argument("--world", type=int, default=1)
 ap.add_argument("--steps", type=int, default=48)
 ap.add_argument("--out", default=None)
+ap.add_argument("--rank", type=int, default=0, help="the shard of --world to profile")
 a = ap.parse_args()
 dt, hh = 4, 12
 days = math.ceil((math.ceil(a.steps / dt) + hh + 2) / 24) + 1
 homes = synthetic_homes(a.homes, seed=12, days=days, dt=dt, horizon_hours=hh)
 oat, ghi, tou = synthetic_weather(days, dt, math.ceil(a.steps / dt), seed=3, month=7)
 agg = DeviceAggregator(homes, oat, ghi, tou, 0, a.steps, reward_price=[0.0], seed=12, keep_history=False,
-                       rank=0, world=a.world)
+                       rank=a.rank, world=a.world)
 N, H = agg.batch.N, agg.batch.H
 par = ((N * H * 336 * 2 + 255) // 256) * 256
 acc = []
@@ -56,7 +57,12 @@ res = {"homes": N, "world": a.world, "steps": a.steps,
        "bound_greedy_cycles_per_solve_mean": float(acc[:, 8].mean()),
        "bound_rows_per_solve_mean": None,
        "trigger_share_of_dp_slowest1pct": float(acc[slow, 6].sum() / max(1.0, tot[slow].sum())),
-       "dp_cycles_per_solve_pct": {str(q): float(np.percentile(tot, q)) for q in (50, 90, 99, 100)}}
+       "dp_cycles_per_solve_pct": {str(q): float(np.percentile(tot, q)) for q in (50, 90, 99, 100)},
+       "slowest_solve": {"sections": dict(zip(names, acc[int(np.argmax(tot)), :5].round(0).tolist())),
+                         "stages": float(acc[int(np.argmax(tot)), 5]),
+                         "trigger": float(acc[int(np.argmax(tot)), 6]),
+                         "bound_backward": float(acc[int(np.argmax(tot)), 7]),
+                         "bound_greedy": float(acc[int(np.argmax(tot)), 8])}}
 print(json.dumps(res, indent=1))
 if a.out:
     json.dump(res, open(a.out, "w"), indent=1)
