@@ -1058,7 +1058,8 @@ DEV bool dp_chain(const Home& h, const Lds& L, const DpChain& c, int lane) {
     return true;
 }
 
-template <int SS, int CAP = NF, int CAPB = NF_BOUND, int PS = NB_CAP, int NBK = NTB, int NW = 1, bool CELL = false>
+template <int SS, int CAP = NF, int CAPB = NF_BOUND, int PS = NB_CAP, int NBK = NTB, int NW = 1, bool CELL = false,
+          int ILP = 1>
 DEV int dp_front(const struct FrontBufs& B, int H, int tid, double g, double x0, double lo0, double hi0, double lo,
                  double hi, int sx, int sv, bool use_bound = false, double ub_ext = INFINITY,
                  double* best_out = nullptr, int beam_k = 0);
@@ -2406,6 +2407,17 @@ DEV double w_eval(const FrontBufs& B, double x, int st0) {
         if (B.wlx[i + st] <= x) i += st;
     return fma(x - B.wlx[i], B.wls[i], B.wlv[i]);
 }
+// two points' W in lockstep (the same search depth): the same values as two w_eval calls
+DEV void w_eval2(const FrontBufs& B, double x, double y, int st0, double& wx, double& wy) {
+    int i = 0, j = 0;
+    for (int st = st0; st > 0; st >>= 1) {
+        const double a = B.wlx[i + st], b = B.wlx[j + st];
+        if (a <= x) i += st;
+        if (b <= y) j += st;
+    }
+    wx = fma(x - B.wlx[i], B.wls[i], B.wlv[i]);
+    wy = fma(y - B.wlx[j], B.wls[j], B.wlv[j]);
+}
 // inclusive scan over the 64 lanes with identity id (lanes shifted in from outside a row
 // keep id: bound_ctrl off), rows combined through v_readlane
 template <int CTRL, typename T>
@@ -2557,9 +2569,12 @@ DEV bool cell_rows(float* cg, float* r0, float* r1, const double* cA, const doub
     return true;
 }
 
-template <int SS, int CAP, int CAPB, int PS, int NBK, int NW, bool CELL>
+template <int SS, int CAP, int CAPB, int PS, int NBK, int NW, bool CELL, int ILP>
 DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double lo0, double hi0, double lo,
                  double hi, int sx, int sv, bool use_bound, double ub_ext, double* best_out, int beam_k) {
+    // ILP = 2 (one wave, few homes per GPU: the launch is as long as its slowest home): passes 1 and 3 take
+    // two 64-child chunks per iteration, so that their LDS round trips overlap; same children, same order
+    static_assert(ILP == 1 || (ILP == 2 && NW == 1), "two chunks per pass on one wave only");
     // NW waves share one home's DP (latency: few homes per GPU): every wave runs the same
     // uniform control flow (W table, hulls and scans are computed redundantly or by wave 0), the
     // children of a stage are split into contiguous pass ranges per wave, and survivors keep the
@@ -2783,6 +2798,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     auto bound_at = [&](double x, int wst_) -> double {
         if constexpr (CELL) return cell_at(x); else return w_eval(B, x, wst_);
     };
+    auto bound_at2 = [&](double x, double y, int wst_, double& bx_, double& by_) {
+        if constexpr (CELL) { bx_ = cell_at(x); by_ = cell_at(y); } else w_eval2(B, x, y, wst_, bx_, by_);
+    };
     // the front stores each label's exact STATE x (not its key dx * x) and cost
     double2* fa = B.fa;
     double2* fb = B.fb;
@@ -2898,16 +2916,38 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         // 1. per key bucket the cheapest child (largest key among equally cheap ones), per
         //    cost bucket the largest-key child (cheapest among equal keys), both as
         //    understated bounds (cost up, key down), by 64-bit LDS atomics
-        for (int c = tid; c < nc && !nodom; c += NT) {
-            const int i = c / NU, u = c - i * NU;
-            const double2 Li = fa[i];
-            const double xc = fma(A, Li.x, fma(g, (double)u, C));
-            const double cc = fma(q, (double)u, Li.y);
-            if (xc >= bl && xc <= bh && (!prune || cc + bound_at(xc, wst) <= UBT)) {
-                const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
-                const unsigned cu = vc + 2u, kd = dn(vk);
-                atomicMin(&B.kb[min(NBK - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
-                atomicMax(&B.cb[min(NBK - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
+        auto bucket_refs = [&](double xc, double cc) {
+            const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
+            const unsigned cu = vc + 2u, kd = dn(vk);
+            atomicMin(&B.kb[min(NBK - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
+            atomicMax(&B.cb[min(NBK - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
+        };
+        if constexpr (ILP == 2) {
+            for (int c = tid; c < nc && !nodom; c += 2 * NT) {
+                const int c2 = c + NT;
+                const bool h2 = c2 < nc;
+                const int i = c / NU, u = c - i * NU;
+                const int i2 = h2 ? c2 / NU : i, u2 = h2 ? c2 - i2 * NU : u;
+                const double2 Li = fa[i], L2 = fa[i2];
+                const double xc = fma(A, Li.x, fma(g, (double)u, C)), x2 = fma(A, L2.x, fma(g, (double)u2, C));
+                const double cc = fma(q, (double)u, Li.y), c2c = fma(q, (double)u2, L2.y);
+                bool k1 = xc >= bl && xc <= bh, k2 = h2 && x2 >= bl && x2 <= bh;
+                if (prune) {
+                    double b1, b2;
+                    bound_at2(xc, x2, wst, b1, b2);
+                    k1 = k1 && cc + b1 <= UBT;
+                    k2 = k2 && c2c + b2 <= UBT;
+                }
+                if (k1) bucket_refs(xc, cc);
+                if (k2) bucket_refs(x2, c2c);
+            }
+        } else {
+            for (int c = tid; c < nc && !nodom; c += NT) {
+                const int i = c / NU, u = c - i * NU;
+                const double2 Li = fa[i];
+                const double xc = fma(A, Li.x, fma(g, (double)u, C));
+                const double cc = fma(q, (double)u, Li.y);
+                if (xc >= bl && xc <= bh && (!prune || cc + bound_at(xc, wst) <= UBT)) bucket_refs(xc, cc);
             }
         }
         __syncthreads();
@@ -2958,7 +2998,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         int nn = 0;
         unsigned kmn = ~0u, kmx = 0u, cmn = ~0u, cmx = 0u;  // survivors' fixed-point ranges
         // child c of this stage: state, cost, fixed-point positions and the keep decision
-        auto eval = [&](int c, int& i, int& u, double& xc, double& cc, unsigned& vk, unsigned& vc) -> bool {
+        auto child = [&](int c, int& i, int& u, double& xc, double& cc, unsigned& vk, unsigned& vc) -> bool {
             const bool have = c < nc;
             i = have ? c / NU : 0;
             u = c - i * NU;
@@ -2967,7 +3007,22 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             cc = fma(q, (double)u, Li.y);
             vk = fixp(fma(xc, kmul, kadd));
             vc = fixp(fma(cc, csc, cadd));
-            bool keep = have && xc >= bl && xc <= bh;
+            return have && xc >= bl && xc <= bh;
+        };
+        auto undominated = [&](unsigned vk, unsigned vc) -> bool {
+            const int kbk = min(NBK - 1, (int)(vk >> 23)), cbk = min(NBK - 1, (int)(vc >> 23));
+            const unsigned ku = vk + 2u, cd = dn(vc);
+            const unsigned long long ky = B.kb[kbk], cy = B.cb[cbk];
+            const unsigned ycu = (unsigned)(ky >> 32), ykd = ~(unsigned)ky;
+            const unsigned zkd = (unsigned)(cy >> 32), zcu = ~(unsigned)cy;
+            const bool d1 = cd >= B.mh[kbk];
+            const bool d2 = ku <= ykd && cd >= ycu && (ku < ykd || cd > ycu);
+            const bool d3 = ku <= B.kl[cbk];
+            const bool d4 = ku <= zkd && cd >= zcu && (ku < zkd || cd > zcu);
+            return !(d1 || d2 || d3 || d4);
+        };
+        auto eval = [&](int c, int& i, int& u, double& xc, double& cc, unsigned& vk, unsigned& vc) -> bool {
+            bool keep = child(c, i, u, xc, cc, vk, vc);
             if (keep && prune) keep = cc + bound_at(xc, wst) <= UBT;
             if (keep && !nodom) {
                 const int kbk = min(NBK - 1, (int)(vk >> 23)), cbk = min(NBK - 1, (int)(vc >> 23));
@@ -2984,7 +3039,41 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             return keep;
         };
         unsigned Kmn, Kmx, Cmn, Cmx;
-        if constexpr (NW == 1) {
+        auto append = [&](bool keep, int i, int u, double xc, double cc, unsigned vk, unsigned vc) {
+            const unsigned long long bal = __ballot(keep);
+            const int slot = nn + __popcll(bal & below);
+            nn += __popcll(bal);
+            if (keep && slot < capn) {
+                fb[slot] = make_double2(xc, cc);
+                B.par[k * PS + slot] = (uint16_t)(i | (u << 12));
+                kmn = umin(kmn, vk); kmx = umax(kmx, vk);
+                cmn = umin(cmn, vc); cmx = umax(cmx, vc);
+            }
+        };
+        if constexpr (ILP == 2) {
+            for (int c0 = 0; c0 < nc; c0 += 2 * WAVE) {
+                int i, u, i2, u2;
+                double xc, cc, x2, c2c;
+                unsigned vk, vc, vk2, vc2;
+                bool k1 = child(c0 + lane, i, u, xc, cc, vk, vc);
+                bool k2 = child(c0 + WAVE + lane, i2, u2, x2, c2c, vk2, vc2);
+                if (prune) {
+                    double b1, b2;
+                    bound_at2(xc, x2, wst, b1, b2);
+                    k1 = k1 && cc + b1 <= UBT;
+                    k2 = k2 && c2c + b2 <= UBT;
+                }
+                if (!nodom) {
+                    const bool n1 = undominated(vk, vc), n2 = undominated(vk2, vc2);
+                    k1 = k1 && n1;
+                    k2 = k2 && n2;
+                }
+                append(k1, i, u, xc, cc, vk, vc);
+                append(k2, i2, u2, x2, c2c, vk2, vc2);
+            }
+            Kmn = dpp_reduce(kmn, umin); Kmx = dpp_reduce(kmx, umax);
+            Cmn = dpp_reduce(cmn, umin); Cmx = dpp_reduce(cmx, umax);
+        } else if constexpr (NW == 1) {
             for (int c0 = 0; c0 < nc; c0 += WAVE) {
                 int i, u;
                 double xc, cc;
@@ -4094,7 +4183,7 @@ constexpr int BK_OK = 1 << 28;           // the bucketed DP found a schedule (in
 constexpr int BK_DONE = 1 << 29;         // the bucketed DP already ran for the deferred chain (mid -> big)
 constexpr int BK_BEAM = (int)(1u << 31); // ... and that schedule is the beam pass's (diagnostic: int_path bit 17)
 
-template <bool EXPLICIT, int MODE, int NW = 1>
+template <bool EXPLICIT, int MODE, int NW = 1, int ILP = 1>
 DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int first_chain, int eflags = 0) {
     constexpr bool SECOND = MODE == DM_BUCKET || MODE == DM_MID;   // the bucketed DP + an exact big-front pass
     constexpr int NT = NW * WAVE;
@@ -4341,7 +4430,8 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 const FrontBufs FB{D.lab, D.rmin, D.kb, D.cb, D.mh, D.kl, D.flo, D.fhi, D.cA, D.cC, D.cq, D.x, D.par,
                                    wg, wl, wl + WAVE, wl + 2 * WAVE, xch};
                 if constexpr (MODE == DM_FRONT)
-                    r = dp_front<6, NF_HOT, NF_HOT, NB_CAP, NTB_HOT, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
+                    r = dp_front<6, NF_HOT, NF_HOT, NB_CAP, NTB_HOT, NW, false, ILP>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv,
+                                                                                   use_bound);
                 else
                     r = dp_front<6, NF, NF_BOUND, NB_CAP, NTB, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
 #ifdef DRAGG_FRONT_STATS2
@@ -4531,8 +4621,8 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
     lag_finish(a, home);
 }
 
-template <bool EXPLICIT, int MODE, int NW = 1>
-__global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW ? 1 : 2) void mpc_direct_kernel(KArgs a) {
+template <bool EXPLICIT, int MODE, int NW = 1, int ILP = 1>
+__global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? (ILP > 1 ? 2 : 3) : MODE == DM_NARROW ? 1 : 2) void mpc_direct_kernel(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     char* const ws = a.lws ? a.lws : reinterpret_cast<char*>(a.p.workspace);
     const int N = a.d.n_homes, H = a.d.horizon;
@@ -4551,7 +4641,7 @@ __global__ __launch_bounds__(WAVE * NW, MODE == DM_FRONT ? 3 : MODE == DM_NARROW
             }
             if (c & LAG_SIDE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the side pass's rows
         }
-        solve_direct<EXPLICIT, MODE, NW>(a, home, smem, 0, 0);
+        solve_direct<EXPLICIT, MODE, NW, ILP>(a, home, smem, 0, 0);
         return;
     }
     // persistent: block b solves listed home b first, then takes the next ones off a shared counter
@@ -4634,8 +4724,9 @@ __global__ __launch_bounds__(NT_CELL, 4) void cell_kernel(KArgs a) {
 }
 
 // lag mode, the side pass's hot launch: a persistent consumer of the homes the main pass skipped (its own
-// kernel, so that the main pass's hot kernel keeps its registers: one inlined solve, no list loop)
-__global__ __launch_bounds__(WAVE, 3) void side_front_kernel(KArgs a) {
+// kernel, so that the main pass's hot kernel keeps its registers: one inlined solve, no list loop; two chunks
+// per front-DP pass and two waves per SIMD: it holds a lagging home or two, whose latency is its time)
+__global__ __launch_bounds__(WAVE, 2) void side_front_kernel(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = a.d.n_homes;
     int* const list = a.hot_list;
@@ -4643,7 +4734,7 @@ __global__ __launch_bounds__(WAVE, 3) void side_front_kernel(KArgs a) {
     __shared__ int take;
     for (int j = blockIdx.x; j < cnt;) {
         const int home = list[j] & HOME_MASK;
-        if (home < N) solve_direct<false, DM_FRONT, 1>(a, home, smem, blockIdx.x, 0, 0);
+        if (home < N) solve_direct<false, DM_FRONT, 1, 2>(a, home, smem, blockIdx.x, 0, 0);
         __syncthreads();
         if (threadIdx.x == 0) take = (int)gridDim.x + atomicAdd(list + N + 1, 1);
         __syncthreads();
@@ -4771,6 +4862,7 @@ struct Knobs {
     int step_pool_cap = POOL_CAP;     // DRAGG_STEP_POOL_CAP: a smaller step-function DP pool (tests of its
     long long step_work_cap = 0;      //   capacity path); DRAGG_STEP_WORK_CAP: its work bound (0: default)
     int side_grid[4] = {0, 0, 0, 0};  // DRAGG_SIDE_GRID=hot,mid,big,narrow: the side pass's blocks (A/B)
+    int ilp = 0;                      // DRAGG_HOT_ILP=1|2: the hot launch's chunks per pass (0: by N, hot_ilp)
 };
 Knobs read_knobs() {
     Knobs r;
@@ -4784,6 +4876,8 @@ Knobs read_knobs() {
     if (wc && atoll(wc) > 0) r.step_work_cap = atoll(wc);
     const char* sg = getenv("DRAGG_SIDE_GRID");
     if (sg) sscanf(sg, "%d,%d,%d,%d", &r.side_grid[0], &r.side_grid[1], &r.side_grid[2], &r.side_grid[3]);
+    const char* il = getenv("DRAGG_HOT_ILP");
+    if (il && (il[0] == '1' || il[0] == '2') && il[1] == 0) r.ilp = il[0] - '0';
     return r;
 }
 Knobs g_knobs = read_knobs();          // at library load; again only on dragg_mpc_reload_knobs()
@@ -4794,6 +4888,19 @@ const Knobs& knobs() { return g_knobs; }
 // scans, barriers) dominates its passes at these front sizes, so extra waves only add barriers);
 // DRAGG_WAVES_PER_HOME forces 2 or 4 (bit-identical results).
 int hot_waves() { return knobs().waves; }
+
+// Chunks per front-DP pass of the one-wave hot launch: two when the homes fit in two waves per SIMD
+// (N <= 8 per CU: the launch then lasts as long as its slowest home, whose LDS round trips the second
+// chunk overlaps), else one (three waves per SIMD hide them; the second chunk's registers would cost one)
+int hot_ilp(int dev, int N) {
+    if (knobs().ilp) return knobs().ilp;
+    static int cus[MAX_DEV] = {};
+    if (!cus[dev]) {
+        hipDeviceProp_t prop{};
+        cus[dev] = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+    }
+    return N <= 8 * cus[dev] ? 2 : 1;
+}
 
 // blocks of the persistent mid launch: as many as the GPU holds at once at its LDS (<= MID_SLOTS_MAX),
 // cached per (device, LDS bytes): a batch with another horizon gets its own occupancy
@@ -4820,7 +4927,7 @@ int mid_slots(int dev, int H, int S) {
 
 template <bool EXPLICIT>
 int launch(const KArgs& a, hipStream_t s) {
-    static int attr_dev[MAX_DEV][8] = {};
+    static int attr_dev[MAX_DEV][10] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return DRAGG_E_HIP;
     int* const attr = attr_dev[dev];
@@ -4845,7 +4952,8 @@ int launch(const KArgs& a, hipStream_t s) {
 
     const int rc = nw == 4 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 4>, attr[4], b, N, 4 * WAVE, lds, s)
                  : nw == 2 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 2>, attr[3], b, N, 2 * WAVE, lds, s)
-                           : launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 1>, attr[1], b, N, WAVE, lds, s);
+                 : hot_ilp(dev, N) == 2 ? launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 1, 2>, attr[8], b, N, WAVE, lds, s)
+                                        : launch_kernel(mpc_direct_kernel<EXPLICIT, DM_FRONT, 1>, attr[1], b, N, WAVE, lds, s);
     if (rc) return rc;
     // RL prices possible (a reward-price list): the cell bound of the deferred homes' indoor-air chains
     if (a.d.n_rp > 1) {
@@ -4886,7 +4994,7 @@ constexpr int SIDE_MID_BLOCKS = 16;         // ... mid launch
 constexpr int SIDE_BIG_BLOCKS = 16;         // ... big launch
 constexpr int SIDE_NARROW_BLOCKS = 2;       // ... step-function launch (each needs a whole CU's LDS)
 int launch_lag(const KArgs& a, bool side, hipStream_t s) {
-    static int attr_dev[MAX_DEV][8] = {};
+    static int attr_dev[MAX_DEV][10] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return DRAGG_E_HIP;
     int* const attr = attr_dev[dev];
@@ -4905,7 +5013,8 @@ int launch_lag(const KArgs& a, bool side, hipStream_t s) {
         if (hipGetLastError() != hipSuccess) return DRAGG_E_HIP;
         b.hot_list = nullptr;
         b.side = 0;
-        int rc = launch_kernel(mpc_direct_kernel<false, DM_FRONT, 1>, attr[1], b, N, WAVE, lds, s);
+        int rc = hot_ilp(dev, N) == 2 ? launch_kernel(mpc_direct_kernel<false, DM_FRONT, 1, 2>, attr[8], b, N, WAVE, lds, s)
+                                      : launch_kernel(mpc_direct_kernel<false, DM_FRONT, 1>, attr[1], b, N, WAVE, lds, s);
         if (!rc && a.d.n_rp > 1)
             rc = launch_kernel(cell_kernel, attr[7], b, min(N, CELL_BLOCKS), NT_CELL, (size_t)cell_lds_bytes(H), s);
         if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_MID, NW_MID>, attr[6], b,
