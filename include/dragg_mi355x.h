@@ -267,7 +267,10 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
 /* Diagnostic knobs, read from the environment when the library loads and again only here (never
    per step): DRAGG_WAVES_PER_HOME=1|2|4 (the hot launch's waves per home; results bit-identical) and
    DRAGG_FORCE_STEP_DP=1 (every chain through the step-function DP; tests), DRAGG_STEP_POOL_CAP=n and
-   DRAGG_STEP_WORK_CAP=n (a smaller pool / work bound of that DP; tests of its capacity path).  Unset: the defaults. */
+   DRAGG_STEP_WORK_CAP=n (a smaller pool / work bound of that DP; tests of its capacity path),
+   DRAGG_HOT_ILP=1|2 (64-child chunks per front-DP pass of the one-wave hot launch; default: 2 at <= 8 homes
+   per CU, else 1; results bit-identical), DRAGG_SIDE_GRID=hot,mid,big,narrow (the lag mode's side-pass
+   grids).  Unset: the defaults. */
 void dragg_mpc_reload_knobs(void);
 
 /* Fill `info` for these dims (needs a GPU: queries the current device). */
