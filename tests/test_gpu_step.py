@@ -213,8 +213,10 @@ def test_ecos_solver_every_solve_falls_back(gpu):
 def test_waves_per_home_bit_identical(gpu):
     """The hot launch's waves per home (1 for throughput; 2 or 4 when the homes all fit on the GPU
     at once, a strong-scaling shard) split each DP stage's children over the waves but keep the
-    single-wave order: 12 closed-loop steps of 1,500 homes of the bench community (H = 48, July,
-    TOU: tariff boundaries, LP-bound pruning) give the same hash, status and objective bit for bit."""
+    single-wave order, and so do one wave's two 64-child chunks per pass (DRAGG_HOT_ILP=2, the default
+    at <= 8 homes per CU, as here) against one: 12 closed-loop steps of 1,500 homes of the bench
+    community (H = 48, July, TOU: tariff boundaries, LP-bound pruning) give the same hash, status and
+    objective bit for bit."""
     import math
     import os
     import torch
@@ -227,8 +229,10 @@ def test_waves_per_home_bit_identical(gpu):
     oat, ghi, tou = synthetic_weather(days, dt, math.ceil(steps / dt), seed=3, month=7)
     out = {}
     try:
-        for nw in ("1", "2", "4"):
-            os.environ["DRAGG_WAVES_PER_HOME"] = nw
+        for nw in ("1", "2", "4", "1/ilp1"):
+            os.environ["DRAGG_WAVES_PER_HOME"] = nw[0]
+            if nw.endswith("ilp1"):
+                os.environ["DRAGG_HOT_ILP"] = "1"
             L.reload_knobs()                 # (read at library load, never per step)
             agg = DeviceAggregator(homes, oat, ghi, tou, 0, steps, reward_price=[0.0], seed=12)
             for t in range(steps):
@@ -238,7 +242,8 @@ def test_waves_per_home_bit_identical(gpu):
                        agg.batch.obj.nan_to_num(7.5).cpu())
     finally:
         os.environ.pop("DRAGG_WAVES_PER_HOME", None)
+        os.environ.pop("DRAGG_HOT_ILP", None)
         L.reload_knobs()
-    for nw in ("2", "4"):
+    for nw in ("2", "4", "1/ilp1"):
         for a, b in zip(out["1"], out[nw]):
             assert torch.equal(a, b), nw
