@@ -58,6 +58,7 @@ constexpr int MC_CAP = 8 * NP_CAP;        // merged candidate points of one stag
 constexpr int STEP_CH = 8;                // merged outputs per merge work item, at most (fewer on small stages)
 constexpr int LW_ROWS = 256;              // rows of the LP bounds L_k / W_k per slot (H < LW_ROWS)
 constexpr int NF_MID = 384;              // front capacity of the mid launch (DM_MID)
+constexpr int RS_HOLD = 4;               // ILP = 2 front DP: child pairs held in registers from pass 1 to pass 3
 // RL-priced chains (a price change at most stages): the exact front DPs prune by a cell bound -- a lower
 // bound of the INTEGER cost-to-go per cell of a uniform grid over the chain's box (cell_rows), 1-3 %
 // below the optimum where the LP cost-to-go is ~13 % below -- and a beam pass (fronts truncated to the
@@ -2922,22 +2923,43 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             atomicMin(&B.kb[min(NBK - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
             atomicMax(&B.cb[min(NBK - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
         };
+        // ILP = 2: children c and c + NT of a pair; the first RS pairs' states, costs and box / bound verdicts
+        // stay in registers for pass 3 (no second load of their parents, no second bound search)
+        double r_x1[RS_HOLD], r_x2[RS_HOLD], r_c1[RS_HOLD], r_c2[RS_HOLD];
+        unsigned r_keep = 0u;                        // bit 2r: pair r's first child passed, 2r + 1: its second
+        auto pair1 = [&](int c, double& xc, double& cc, double& x2, double& c2c, bool& k1, bool& k2) {
+            const int c2 = c + NT;
+            const bool h1 = c < nc, h2 = c2 < nc;
+            const int i = h1 ? c / NU : 0, u = c - i * NU;
+            const int i2 = h2 ? c2 / NU : i, u2 = h2 ? c2 - i2 * NU : u;
+            const double2 Li = fa[i], L2 = fa[i2];
+            xc = fma(A, Li.x, fma(g, (double)u, C)); x2 = fma(A, L2.x, fma(g, (double)u2, C));
+            cc = fma(q, (double)u, Li.y); c2c = fma(q, (double)u2, L2.y);
+            k1 = h1 && xc >= bl && xc <= bh; k2 = h2 && x2 >= bl && x2 <= bh;
+            if (prune) {
+                double b1, b2;
+                bound_at2(xc, x2, wst, b1, b2);
+                k1 = k1 && cc + b1 <= UBT;
+                k2 = k2 && c2c + b2 <= UBT;
+            }
+        };
         if constexpr (ILP == 2) {
-            for (int c = tid; c < nc && !nodom; c += 2 * NT) {
-                const int c2 = c + NT;
-                const bool h2 = c2 < nc;
-                const int i = c / NU, u = c - i * NU;
-                const int i2 = h2 ? c2 / NU : i, u2 = h2 ? c2 - i2 * NU : u;
-                const double2 Li = fa[i], L2 = fa[i2];
-                const double xc = fma(A, Li.x, fma(g, (double)u, C)), x2 = fma(A, L2.x, fma(g, (double)u2, C));
-                const double cc = fma(q, (double)u, Li.y), c2c = fma(q, (double)u2, L2.y);
-                bool k1 = xc >= bl && xc <= bh, k2 = h2 && x2 >= bl && x2 <= bh;
-                if (prune) {
-                    double b1, b2;
-                    bound_at2(xc, x2, wst, b1, b2);
-                    k1 = k1 && cc + b1 <= UBT;
-                    k2 = k2 && c2c + b2 <= UBT;
+#pragma unroll
+            for (int r = 0; r < RS_HOLD; ++r) {
+                if (r * 2 * NT < nc && !nodom) {
+                    double xc, cc, x2, c2c;
+                    bool k1, k2;
+                    pair1(tid + r * 2 * NT, xc, cc, x2, c2c, k1, k2);
+                    r_x1[r] = xc; r_c1[r] = cc; r_x2[r] = x2; r_c2[r] = c2c;
+                    r_keep |= (k1 ? 1u : 0u) << (2 * r) | (k2 ? 2u : 0u) << (2 * r);
+                    if (k1) bucket_refs(xc, cc);
+                    if (k2) bucket_refs(x2, c2c);
                 }
+            }
+            for (int c = tid + RS_HOLD * 2 * NT; c < nc && !nodom; c += 2 * NT) {
+                double xc, cc, x2, c2c;
+                bool k1, k2;
+                pair1(c, xc, cc, x2, c2c, k1, k2);
                 if (k1) bucket_refs(xc, cc);
                 if (k2) bucket_refs(x2, c2c);
             }
@@ -3051,7 +3073,19 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             }
         };
         if constexpr (ILP == 2) {
-            for (int c0 = 0; c0 < nc; c0 += 2 * WAVE) {
+            auto pair3 = [&](int c0, int i, int u, int i2, int u2, double xc, double cc, double x2, double c2c, bool k1,
+                             bool k2) {
+                const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
+                const unsigned vk2 = fixp(fma(x2, kmul, kadd)), vc2 = fixp(fma(c2c, csc, cadd));
+                if (!nodom) {
+                    const bool n1 = undominated(vk, vc), n2 = undominated(vk2, vc2);
+                    k1 = k1 && n1;
+                    k2 = k2 && n2;
+                }
+                append(k1, i, u, xc, cc, vk, vc);
+                append(k2, i2, u2, x2, c2c, vk2, vc2);
+            };
+            auto fresh = [&](int c0) {
                 int i, u, i2, u2;
                 double xc, cc, x2, c2c;
                 unsigned vk, vc, vk2, vc2;
@@ -3063,14 +3097,23 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     k1 = k1 && cc + b1 <= UBT;
                     k2 = k2 && c2c + b2 <= UBT;
                 }
-                if (!nodom) {
-                    const bool n1 = undominated(vk, vc), n2 = undominated(vk2, vc2);
-                    k1 = k1 && n1;
-                    k2 = k2 && n2;
+                pair3(c0, i, u, i2, u2, xc, cc, x2, c2c, k1, k2);
+            };
+#pragma unroll
+            for (int r = 0; r < RS_HOLD; ++r) {
+                const int c0 = r * 2 * WAVE;
+                if (c0 < nc) {
+                    if (!nodom) {                       // pass 1's children (the same arithmetic, kept)
+                        const int c = c0 + lane, c2 = c + WAVE;
+                        const int i = c < nc ? c / NU : 0, i2 = c2 < nc ? c2 / NU : i;
+                        pair3(c0, i, c - i * NU, i2, c2 < nc ? c2 - i2 * NU : c - i * NU, r_x1[r], r_c1[r], r_x2[r],
+                              r_c2[r], (r_keep >> (2 * r)) & 1u, (r_keep >> (2 * r + 1)) & 1u);
+                    } else {
+                        fresh(c0);
+                    }
                 }
-                append(k1, i, u, xc, cc, vk, vc);
-                append(k2, i2, u2, x2, c2c, vk2, vc2);
             }
+            for (int c0 = RS_HOLD * 2 * WAVE; c0 < nc; c0 += 2 * WAVE) fresh(c0);
             Kmn = dpp_reduce(kmn, umin); Kmx = dpp_reduce(kmx, umax);
             Cmn = dpp_reduce(cmn, umin); Cmx = dpp_reduce(cmx, umax);
         } else if constexpr (NW == 1) {
