@@ -1,5 +1,5 @@
 """The committed measurement is reproducible from the committed profiles:
-profiles/r03/traffic_*.json recompute from the raw rocprofv3 passes under profiles/r03/*_prof
+profiles/r0{3,5}/traffic_*.json recompute from the raw rocprofv3 passes under profiles/r0{3,5}/*_prof
 (tools/make_traffic.py), and the committed bench lines' kernel time and derived rooflines agree with
 the profile of the same command and window (within 5 %)."""
 import json
@@ -10,16 +10,19 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-P = os.path.join(ROOT, "profiles", "r03")
+ARGS = {
+    "driver": ["--steps", "20", "--warmup", "5"],
+    "rl": ["--steps", "6", "--warmup", "1", "--workload", "rl", "--rl-price", "smooth", "--forecast-horizon", "1"],
+}
+# (round, the bench line of each workload measured on that round's build)
+ROUNDS = {"r03": "bench_{}_line.json", "r05": os.path.join("lines", "{}.json")}
 
-CASES = [
-    ("driver", ["--steps", "20", "--warmup", "5"]),
-    ("rl", ["--steps", "6", "--warmup", "1", "--workload", "rl", "--rl-price", "smooth", "--forecast-horizon", "1"]),
-]
 
-
-@pytest.mark.parametrize("name,args", CASES)
-def test_traffic_recomputes_from_raw_passes(name, args, tmp_path):
+@pytest.mark.parametrize("rnd", sorted(ROUNDS))
+@pytest.mark.parametrize("name", sorted(ARGS))
+def test_traffic_recomputes_from_raw_passes(rnd, name, tmp_path):
+    P = os.path.join(ROOT, "profiles", rnd)
+    args = ARGS[name]
     prof = os.path.join(P, f"{name}_prof")
     if not os.path.isdir(prof):
         pytest.skip("no raw profile passes")
@@ -35,11 +38,13 @@ def test_traffic_recomputes_from_raw_passes(name, args, tmp_path):
         assert got["sq_per_step"][k] == pytest.approx(v, rel=1e-12), k
 
 
-@pytest.mark.parametrize("name", ["driver", "rl"])
-def test_bench_line_agrees_with_its_profile(name):
+@pytest.mark.parametrize("rnd", sorted(ROUNDS))
+@pytest.mark.parametrize("name", sorted(ARGS))
+def test_bench_line_agrees_with_its_profile(rnd, name):
     sys.path.insert(0, ROOT)
     import bench
-    line = json.load(open(os.path.join(P, f"bench_{name}_line.json")))
+    P = os.path.join(ROOT, "profiles", rnd)
+    line = json.load(open(os.path.join(P, ROUNDS[rnd].format(name))))
     tj = json.load(open(os.path.join(P, f"traffic_{name}.json")))
     r = line["roofline"]
     assert r["profile_key"] == tj["workload"]                     # the same command and window
