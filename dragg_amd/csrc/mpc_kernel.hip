@@ -1563,10 +1563,10 @@ __host__ __device__ inline DirectLayout front_layout(int H) {
     o.lab = take(16 * NF_HOT, 16);
     o.rmin = take(16 * NF_HOT, 16);
     o.wl = take(8 * 3 * WAVE, 16);
-    o.kb = take(8 * NTB_HOT, 16);
-    o.cb = take(8 * NTB_HOT, 16);
-    o.mh = take(4 * NTB_HOT, 4);
-    o.kl = take(4 * NTB_HOT, 4);
+    o.kb = take(16 * NTB_HOT, 16);                  // per bucket {key ref u64, mh u32, pad}: one 16-B load
+    o.cb = take(16 * NTB_HOT, 16);                  // per bucket {cost ref u64, kl u32, pad}
+    o.mh = o.kb + 8;
+    o.kl = o.cb + 8;
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
     o.xch = take(xch_bytes(NF_HOT), 16);
@@ -1606,10 +1606,10 @@ __host__ __device__ inline DirectLayout direct_layout(int H, int S) {
     o.rmin = take(16 * (NB_CAP + 8), 16);
     o.tail = p;
     // dp_front tail
-    o.kb = take(8 * NTB, 16);
-    o.cb = take(8 * NTB, 16);
-    o.mh = take(4 * NTB, 4);
-    o.kl = take(4 * NTB, 4);
+    o.kb = take(16 * NTB, 16);                  // per bucket {key ref u64, mh u32, pad}: one 16-B load
+    o.cb = take(16 * NTB, 16);                  // per bucket {cost ref u64, kl u32, pad}
+    o.mh = o.kb + 8;
+    o.kl = o.cb + 8;
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
     const int end_front = p;
@@ -1670,10 +1670,10 @@ __host__ __device__ inline BigLayout big_layout(int H, int S) {
     o.fa = take(16 * NF_BIG, 16);
     o.fb = take(16 * NF_BIG, 16);
     o.wl = take(8 * 3 * WAVE, 16);
-    o.kb = take(8 * NTB_BIG, 16);
-    o.cb = take(8 * NTB_BIG, 16);
-    o.mh = take(4 * NTB_BIG, 4);
-    o.kl = take(4 * NTB_BIG, 4);
+    o.kb = take(16 * NTB_BIG, 16);                  // per bucket {key ref u64, mh u32, pad}: one 16-B load
+    o.cb = take(16 * NTB_BIG, 16);                  // per bucket {cost ref u64, kl u32, pad}
+    o.mh = o.kb + 8;
+    o.kl = o.cb + 8;
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
     p = max(p, d.bytes);                         // past the direct layout too: the regular front DP of
@@ -1692,10 +1692,10 @@ __host__ __device__ inline BigLayout mid_layout(int H, int S) {
     o.fa = take(16 * NF_MID, 16);
     o.fb = take(16 * NF_MID, 16);
     o.wl = take(8 * 3 * WAVE, 16);
-    o.kb = take(8 * NTB_MID, 16);
-    o.cb = take(8 * NTB_MID, 16);
-    o.mh = take(4 * NTB_MID, 4);
-    o.kl = take(4 * NTB_MID, 4);
+    o.kb = take(16 * NTB_MID, 16);                  // per bucket {key ref u64, mh u32, pad}: one 16-B load
+    o.cb = take(16 * NTB_MID, 16);                  // per bucket {cost ref u64, kl u32, pad}
+    o.mh = o.kb + 8;
+    o.kl = o.cb + 8;
     o.flo = take(4 * (H + 1), 4);
     o.fhi = take(4 * (H + 1), 4);
     p = max(p, d.bytes);
@@ -2809,7 +2809,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     int n = 1;
     double xmin = x0, xmax = x0, cmin = 0.0, cmax = 0.0;    // state / cost range of the front
     const unsigned long long below = (1ull << lane) - 1ull;  // lanes < this one
-    for (int b = tid; b < NBK; b += NT) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
+    for (int b = tid; b < NBK; b += NT) { B.kb[2 * b] = ~0ull; B.cb[2 * b] = 0ull; }
     // W_{k+1} of the stage in the LDS table, W_{k+2} in flight
     double2 wnext = make_double2(INFINITY, INFINITY);
     if constexpr (CELL) {
@@ -2920,8 +2920,8 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         auto bucket_refs = [&](double xc, double cc) {
             const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
             const unsigned cu = vc + 2u, kd = dn(vk);
-            atomicMin(&B.kb[min(NBK - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
-            atomicMax(&B.cb[min(NBK - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
+            atomicMin(&B.kb[2 * min(NBK - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
+            atomicMax(&B.cb[2 * min(NBK - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
         };
         // ILP = 2: children c and c + NT of a pair; the first RS pairs' states, costs and box / bound verdicts
         // stay in registers for pass 3 (no second load of their parents, no second bound search)
@@ -2985,9 +2985,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             unsigned lm = ~0u, lk = 0u;
 #pragma unroll
             for (int j = 0; j < BPL; ++j) {
-                bm[j] = (unsigned)(B.kb[c0 + j] >> 32);
+                bm[j] = (unsigned)(B.kb[2 * (c0 + j)] >> 32);
                 lm = umin(lm, bm[j]);
-                bk[j] = (unsigned)(B.cb[d0 + j] >> 32);
+                bk[j] = (unsigned)(B.cb[2 * (d0 + j)] >> 32);
                 lk = umax(lk, bk[j]);
             }
             const unsigned im = dpp_iscan(lm, lane, ~0u, umin);
@@ -2996,12 +2996,12 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             if (lane == 0) { rm = ~0u; rk = 0u; }
 #pragma unroll
             for (int j = BPL - 1; j >= 0; --j) {
-                B.mh[c0 + j] = rm;
+                B.mh[4 * (c0 + j)] = rm;
                 rm = umin(rm, bm[j]);
             }
 #pragma unroll
             for (int j = 0; j < BPL; ++j) {
-                B.kl[d0 + j] = rk;
+                B.kl[4 * (d0 + j)] = rk;
                 rk = umax(rk, bk[j]);
             }
         }
@@ -3034,30 +3034,20 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         auto undominated = [&](unsigned vk, unsigned vc) -> bool {
             const int kbk = min(NBK - 1, (int)(vk >> 23)), cbk = min(NBK - 1, (int)(vc >> 23));
             const unsigned ku = vk + 2u, cd = dn(vc);
-            const unsigned long long ky = B.kb[kbk], cy = B.cb[cbk];
-            const unsigned ycu = (unsigned)(ky >> 32), ykd = ~(unsigned)ky;
-            const unsigned zkd = (unsigned)(cy >> 32), zcu = ~(unsigned)cy;
-            const bool d1 = cd >= B.mh[kbk];
+            // a bucket's reference and its scan value in one 16-B load each
+            const uint4 rk_ = reinterpret_cast<const uint4*>(B.kb)[kbk], rc_ = reinterpret_cast<const uint4*>(B.cb)[cbk];
+            const unsigned ycu = rk_.y, ykd = ~rk_.x;
+            const unsigned zkd = rc_.y, zcu = ~rc_.x;
+            const bool d1 = cd >= rk_.z;
             const bool d2 = ku <= ykd && cd >= ycu && (ku < ykd || cd > ycu);
-            const bool d3 = ku <= B.kl[cbk];
+            const bool d3 = ku <= rc_.z;
             const bool d4 = ku <= zkd && cd >= zcu && (ku < zkd || cd > zcu);
             return !(d1 || d2 || d3 || d4);
         };
         auto eval = [&](int c, int& i, int& u, double& xc, double& cc, unsigned& vk, unsigned& vc) -> bool {
             bool keep = child(c, i, u, xc, cc, vk, vc);
             if (keep && prune) keep = cc + bound_at(xc, wst) <= UBT;
-            if (keep && !nodom) {
-                const int kbk = min(NBK - 1, (int)(vk >> 23)), cbk = min(NBK - 1, (int)(vc >> 23));
-                const unsigned ku = vk + 2u, cd = dn(vc);
-                const unsigned long long ky = B.kb[kbk], cy = B.cb[cbk];
-                const unsigned ycu = (unsigned)(ky >> 32), ykd = ~(unsigned)ky;
-                const unsigned zkd = (unsigned)(cy >> 32), zcu = ~(unsigned)cy;
-                const bool d1 = cd >= B.mh[kbk];
-                const bool d2 = ku <= ykd && cd >= ycu && (ku < ykd || cd > ycu);
-                const bool d3 = ku <= B.kl[cbk];
-                const bool d4 = ku <= zkd && cd >= zcu && (ku < zkd || cd > zcu);
-                keep = !(d1 || d2 || d3 || d4);
-            }
+            if (keep && !nodom) keep = undominated(vk, vc);
             return keep;
         };
         unsigned Kmn, Kmx, Cmn, Cmx;
@@ -3294,7 +3284,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             cmin = c1 - tw(c1);
             cmax = c2 + tw(c2);
         }
-        for (int b = tid; b < NBK && !nodom; b += NT) { B.kb[b] = ~0ull; B.cb[b] = 0ull; }
+        for (int b = tid; b < NBK && !nodom; b += NT) { B.kb[2 * b] = ~0ull; B.cb[2 * b] = 0ull; }
         if constexpr (CELL) {
             crow = B.cg + (size_t)(k + 2) * NCELL;
         } else if (prune && k + 1 < H && wid == 0) {
@@ -3361,10 +3351,10 @@ DEV bool round_duties(const Home& h, const Lds& L, int lane, uint16_t* par) {
     FrontBufs B;
     B.fa = reinterpret_cast<double2*>(f); f += 2 * NF;
     B.fb = reinterpret_cast<double2*>(f); f += 2 * NF;
-    B.kb = reinterpret_cast<unsigned long long*>(f); f += NTB;
-    B.cb = reinterpret_cast<unsigned long long*>(f); f += NTB;
-    B.mh = reinterpret_cast<unsigned*>(f); f += NTB / 2;
-    B.kl = reinterpret_cast<unsigned*>(f); f += NTB / 2;
+    B.kb = reinterpret_cast<unsigned long long*>(f); f += 2 * NTB;     // (bucket records of 16 B, dp_front)
+    B.cb = reinterpret_cast<unsigned long long*>(f); f += 2 * NTB;
+    B.mh = reinterpret_cast<unsigned*>(B.kb) + 2;
+    B.kl = reinterpret_cast<unsigned*>(B.cb) + 2;
     B.flo = reinterpret_cast<unsigned*>(f); f += (H + 2) / 2;
     B.fhi = reinterpret_cast<unsigned*>(f); f += (H + 2) / 2;
     B.cA = cA; B.cC = cC; B.cq = cq; B.x = L.x; B.par = par;
