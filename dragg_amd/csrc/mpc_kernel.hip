@@ -2917,15 +2917,16 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         // 1. per key bucket the cheapest child (largest key among equally cheap ones), per
         //    cost bucket the largest-key child (cheapest among equal keys), both as
         //    understated bounds (cost up, key down), by 64-bit LDS atomics
-        auto bucket_refs = [&](double xc, double cc) {
-            const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
+        auto bucket_refs_v = [&](unsigned vk, unsigned vc) {
             const unsigned cu = vc + 2u, kd = dn(vk);
             atomicMin(&B.kb[2 * min(NBK - 1, (int)(vk >> 23))], ((unsigned long long)cu << 32) | (unsigned long long)(~kd));
             atomicMax(&B.cb[2 * min(NBK - 1, (int)(vc >> 23))], ((unsigned long long)kd << 32) | (unsigned long long)(~cu));
         };
+        auto bucket_refs = [&](double xc, double cc) { bucket_refs_v(fixp(fma(xc, kmul, kadd)), fixp(fma(cc, csc, cadd))); };
         // ILP = 2: children c and c + NT of a pair; the first RS pairs' states, costs and box / bound verdicts
         // stay in registers for pass 3 (no second load of their parents, no second bound search)
         double r_x1[RS_HOLD], r_x2[RS_HOLD], r_c1[RS_HOLD], r_c2[RS_HOLD];
+        unsigned r_v[RS_HOLD][4];                    // and their fixed-point positions (vk, vc of each child)
         unsigned r_keep = 0u;                        // bit 2r: pair r's first child passed, 2r + 1: its second
         auto pair1 = [&](int c, double& xc, double& cc, double& x2, double& c2c, bool& k1, bool& k2) {
             const int c2 = c + NT;
@@ -2952,8 +2953,10 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     pair1(tid + r * 2 * NT, xc, cc, x2, c2c, k1, k2);
                     r_x1[r] = xc; r_c1[r] = cc; r_x2[r] = x2; r_c2[r] = c2c;
                     r_keep |= (k1 ? 1u : 0u) << (2 * r) | (k2 ? 2u : 0u) << (2 * r);
-                    if (k1) bucket_refs(xc, cc);
-                    if (k2) bucket_refs(x2, c2c);
+                    r_v[r][0] = fixp(fma(xc, kmul, kadd)); r_v[r][1] = fixp(fma(cc, csc, cadd));
+                    r_v[r][2] = fixp(fma(x2, kmul, kadd)); r_v[r][3] = fixp(fma(c2c, csc, cadd));
+                    if (k1) bucket_refs_v(r_v[r][0], r_v[r][1]);
+                    if (k2) bucket_refs_v(r_v[r][2], r_v[r][3]);
                 }
             }
             for (int c = tid + RS_HOLD * 2 * NT; c < nc && !nodom; c += 2 * NT) {
@@ -3063,10 +3066,8 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             }
         };
         if constexpr (ILP == 2) {
-            auto pair3 = [&](int c0, int i, int u, int i2, int u2, double xc, double cc, double x2, double c2c, bool k1,
-                             bool k2) {
-                const unsigned vk = fixp(fma(xc, kmul, kadd)), vc = fixp(fma(cc, csc, cadd));
-                const unsigned vk2 = fixp(fma(x2, kmul, kadd)), vc2 = fixp(fma(c2c, csc, cadd));
+            auto pair3 = [&](int i, int u, int i2, int u2, double xc, double cc, double x2, double c2c, unsigned vk,
+                             unsigned vc, unsigned vk2, unsigned vc2, bool k1, bool k2) {
                 if (!nodom) {
                     const bool n1 = undominated(vk, vc), n2 = undominated(vk2, vc2);
                     k1 = k1 && n1;
@@ -3087,7 +3088,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     k1 = k1 && cc + b1 <= UBT;
                     k2 = k2 && c2c + b2 <= UBT;
                 }
-                pair3(c0, i, u, i2, u2, xc, cc, x2, c2c, k1, k2);
+                pair3(i, u, i2, u2, xc, cc, x2, c2c, vk, vc, vk2, vc2, k1, k2);
             };
 #pragma unroll
             for (int r = 0; r < RS_HOLD; ++r) {
@@ -3096,8 +3097,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     if (!nodom) {                       // pass 1's children (the same arithmetic, kept)
                         const int c = c0 + lane, c2 = c + WAVE;
                         const int i = c < nc ? c / NU : 0, i2 = c2 < nc ? c2 / NU : i;
-                        pair3(c0, i, c - i * NU, i2, c2 < nc ? c2 - i2 * NU : c - i * NU, r_x1[r], r_c1[r], r_x2[r],
-                              r_c2[r], (r_keep >> (2 * r)) & 1u, (r_keep >> (2 * r + 1)) & 1u);
+                        pair3(i, c - i * NU, i2, c2 < nc ? c2 - i2 * NU : c - i * NU, r_x1[r], r_c1[r], r_x2[r], r_c2[r],
+                              r_v[r][0], r_v[r][1], r_v[r][2], r_v[r][3], (r_keep >> (2 * r)) & 1u,
+                              (r_keep >> (2 * r + 1)) & 1u);
                     } else {
                         fresh(c0);
                     }

@@ -37,10 +37,11 @@ args_of() {
     h24) echo --horizon-hours 6 --steps 96 --warmup 4 --cpu-seconds 0 ;;
     cfg3) echo --homes 100000 --horizon-hours 6 --steps 24 --warmup 2 --cpu-seconds 0 ;;
     gloo2) echo --gpus 2 --steps 20 --warmup 5 --cpu-seconds 0 ;;
+    gloo2full) echo --gpus 2 --steps 96 --warmup 4 --cpu-seconds 0 ;;
   esac
 }
 run() { name=$1
-  if [ $name = gloo2 ]; then export DRAGG_BENCH_BACKEND=gloo; else unset DRAGG_BENCH_BACKEND; fi
+  if [ "${name#gloo2}" != "$name" ]; then export DRAGG_BENCH_BACKEND=gloo; else unset DRAGG_BENCH_BACKEND; fi
   timeout -k 10 ${LINE_LIMIT:-400} python3 bench.py $(args_of $name) > $OUT/$name.out 2> $OUT/$name.err || { echo "$name failed"; tail -5 $OUT/$name.err; exit 1; }
   grep '^{' $OUT/$name.out | tail -1 > $OUT/$name.json
   python3 -c "
