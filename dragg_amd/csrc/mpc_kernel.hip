@@ -2575,7 +2575,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                  double hi, int sx, int sv, bool use_bound, double ub_ext, double* best_out, int beam_k) {
     // ILP = 2 (one wave, few homes per GPU: the launch is as long as its slowest home): passes 1 and 3 take
     // two 64-child chunks per iteration, so that their LDS round trips overlap; same children, same order
-    static_assert(ILP == 1 || (ILP == 2 && NW == 1), "two chunks per pass on one wave only");
+    // ILP = 3: two chunks, none held (the side pass's hot kernel: its persistent loop leaves no registers)
+    static_assert(ILP == 1 || ((ILP == 2 || ILP == 3) && NW == 1), "two chunks per pass on one wave only");
+    constexpr int HOLD = ILP == 2 ? RS_HOLD : 0;        // child pairs held in registers from pass 1 to pass 3
     // NW waves share one home's DP (latency: few homes per GPU): every wave runs the same
     // uniform control flow (W table, hulls and scans are computed redundantly or by wave 0), the
     // children of a stage are split into contiguous pass ranges per wave, and survivors keep the
@@ -2925,8 +2927,8 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         auto bucket_refs = [&](double xc, double cc) { bucket_refs_v(fixp(fma(xc, kmul, kadd)), fixp(fma(cc, csc, cadd))); };
         // ILP = 2: children c and c + NT of a pair; the first RS pairs' states, costs and box / bound verdicts
         // stay in registers for pass 3 (no second load of their parents, no second bound search)
-        double r_x1[RS_HOLD], r_x2[RS_HOLD], r_c1[RS_HOLD], r_c2[RS_HOLD];
-        unsigned r_v[RS_HOLD][4];                    // and their fixed-point positions (vk, vc of each child)
+        double r_x1[HOLD > 0 ? HOLD : 1], r_x2[HOLD > 0 ? HOLD : 1], r_c1[HOLD > 0 ? HOLD : 1], r_c2[HOLD > 0 ? HOLD : 1];
+        unsigned r_v[HOLD > 0 ? HOLD : 1][4];                    // and their fixed-point positions (vk, vc of each child)
         unsigned r_keep = 0u;                        // bit 2r: pair r's first child passed, 2r + 1: its second
         auto pair1 = [&](int c, double& xc, double& cc, double& x2, double& c2c, bool& k1, bool& k2) {
             const int c2 = c + NT;
@@ -2944,9 +2946,9 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                 k2 = k2 && c2c + b2 <= UBT;
             }
         };
-        if constexpr (ILP == 2) {
+        if constexpr (ILP >= 2) {
 #pragma unroll
-            for (int r = 0; r < RS_HOLD; ++r) {
+            for (int r = 0; r < HOLD; ++r) {
                 if (r * 2 * NT < nc && !nodom) {
                     double xc, cc, x2, c2c;
                     bool k1, k2;
@@ -2959,7 +2961,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     if (k2) bucket_refs_v(r_v[r][2], r_v[r][3]);
                 }
             }
-            for (int c = tid + RS_HOLD * 2 * NT; c < nc && !nodom; c += 2 * NT) {
+            for (int c = tid + HOLD * 2 * NT; c < nc && !nodom; c += 2 * NT) {
                 double xc, cc, x2, c2c;
                 bool k1, k2;
                 pair1(c, xc, cc, x2, c2c, k1, k2);
@@ -3065,7 +3067,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                 cmn = umin(cmn, vc); cmx = umax(cmx, vc);
             }
         };
-        if constexpr (ILP == 2) {
+        if constexpr (ILP >= 2) {
             auto pair3 = [&](int i, int u, int i2, int u2, double xc, double cc, double x2, double c2c, unsigned vk,
                              unsigned vc, unsigned vk2, unsigned vc2, bool k1, bool k2) {
                 if (!nodom) {
@@ -3091,7 +3093,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                 pair3(i, u, i2, u2, xc, cc, x2, c2c, vk, vc, vk2, vc2, k1, k2);
             };
 #pragma unroll
-            for (int r = 0; r < RS_HOLD; ++r) {
+            for (int r = 0; r < HOLD; ++r) {
                 const int c0 = r * 2 * WAVE;
                 if (c0 < nc) {
                     if (!nodom) {                       // pass 1's children (the same arithmetic, kept)
@@ -3105,7 +3107,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     }
                 }
             }
-            for (int c0 = RS_HOLD * 2 * WAVE; c0 < nc; c0 += 2 * WAVE) fresh(c0);
+            for (int c0 = HOLD * 2 * WAVE; c0 < nc; c0 += 2 * WAVE) fresh(c0);
             Kmn = dpp_reduce(kmn, umin); Kmx = dpp_reduce(kmx, umax);
             Cmn = dpp_reduce(cmn, umin); Cmx = dpp_reduce(cmx, umax);
         } else if constexpr (NW == 1) {
@@ -4769,7 +4771,7 @@ __global__ __launch_bounds__(WAVE, 2) void side_front_kernel(KArgs a) {
     __shared__ int take;
     for (int j = blockIdx.x; j < cnt;) {
         const int home = list[j] & HOME_MASK;
-        if (home < N) solve_direct<false, DM_FRONT, 1, 2>(a, home, smem, blockIdx.x, 0, 0);
+        if (home < N) solve_direct<false, DM_FRONT, 1, 3>(a, home, smem, blockIdx.x, 0, 0);
         __syncthreads();
         if (threadIdx.x == 0) take = (int)gridDim.x + atomicAdd(list + N + 1, 1);
         __syncthreads();
