@@ -366,12 +366,28 @@ def occupancy(batch):
 
 
 def traffic_key(n_total, H, dt, month, int_mode, world, workload="rbo", steps=None, warmup=None, rl_price=None,
-                fh=0):
-    """The identity of a profiled command: workload, community, horizon and the timed window."""
+                fh=0, shard_of=0, shard_rank=None, steps_mode=None):
+    """The identity of a profiled command: workload, community, horizon, the timed window, and (since
+    round 6) the shard a --shard-of line times (`shard_rank`: its rank, or "max" for --shard-max) and
+    how the steps run (`steps_mode`: "lag", "serial" or "adaptive").  A line takes counters only from
+    a pass whose key is its own; keys without the last two parts are the profiles of rounds <= 5."""
     w = f"{n_total} homes, H={H}, dt={dt}, month {month}, int_mode={int_mode}, {world} rank(s)"
     if workload == "rl":
         w += f", rl ({rl_price} price, forecast_horizon {fh})"
-    return w + f", timed steps {warmup}..{(warmup or 0) + (steps or 0) - 1}"
+    w += f", timed steps {warmup}..{(warmup or 0) + (steps or 0) - 1}"
+    if shard_of and shard_of > 1:
+        w += f", shard {shard_rank} of {shard_of}"
+    if steps_mode:
+        w += f", {steps_mode} steps"
+    return w
+
+
+def steps_mode(agg):
+    """How the timed steps ran: "lag" (lag mode from the first step), "adaptive" (serial steps until a
+    step hands a chain to the step-function DP, lag mode after), "serial"."""
+    if not agg.overlap:
+        return "serial"
+    return "adaptive" if getattr(agg, "adaptive", False) else "lag"
 
 
 def window(warmup, steps, dt, month, rl):
@@ -576,6 +592,9 @@ def main():
     if world > 1:
         torch.distributed.all_reduce(counts)
     counts = counts.cpu().tolist()
+    # the timed solves' integer paths over every rank (int_path): approximate schedules (bits 0-11), the
+    # step-function DP (bit 15)
+    paths = agg.approx_counts(args.warmup, total_steps)
     # the homes every rank solved (strided shards: the rank's share of the community)
     per_rank = torch.tensor([agg.batch.N], dtype=torch.int64, device="cuda" if backend == "nccl" else "cpu")
     if world > 1:
@@ -587,6 +606,7 @@ def main():
         homes_per_rank, dist_world = [int(agg.batch.N)], 1
     stat_counts = {name: int(c) for name, c in zip(names, counts)}
     success = stat_counts["optimal"] / max(1, sum(stat_counts.values()))
+    stat_counts.update(paths)
     solves = (agg.batch.N if shard else n_total) * args.steps * (1 + fh)
     value = solves / elapsed
     if rank == 0:
@@ -600,7 +620,8 @@ def main():
         alg_bytes = bytes_per_launch(agg.batch, success) * (1 + fh)     # rl: per action (rollouts + commit)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         key = traffic_key(n_total, H, dt, args.month, args.int_mode, world, args.workload, args.steps, args.warmup,
-                          args.rl_price if rl else None, fh)
+                          args.rl_price if rl else None, fh, args.shard_of if shard else 0,
+                          ("max" if shard_times else slow_rank) if shard else None, steps_mode(agg))
         pmc, traffic_src = measured_pmc(key)
         traffic = pmc.get("bytes_per_step")
         out = {
@@ -633,6 +654,7 @@ def main():
             "window": window(args.warmup, args.steps, dt, args.month, rl),
             "history_written": not args.no_history,
             "lag_mode": bool(agg.overlap),
+            "steps_mode": steps_mode(agg),
             "sim_wall_s": elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0,

@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # DRAGG_LIB: an alternative build of the same library (kernel experiments); default in-tree
 LIB_PATH = os.environ.get("DRAGG_LIB") or os.path.join(HERE, "libdragg_mi355x.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # enums (mirror include/dragg_mi355x.h)
 BASE, PV_ONLY, BATTERY_ONLY, PV_BATTERY = 0, 1, 2, 3
@@ -101,7 +101,8 @@ class KernelInfo(ctypes.Structure):
 EXPORTS = ["dragg_mpc_abi_version", "dragg_mpc_strerror", "dragg_mpc_lds_bytes", "dragg_mpc_workspace_bytes",
            "dragg_mpc_kernel_info_get", "dragg_mpc_step",
            "dragg_mpc_solve_explicit", "dragg_mpc_aggregate", "dragg_mpc_season_noise", "dragg_mpc_reload_knobs",
-           "dragg_mpc_lag_reset", "dragg_mpc_step_main", "dragg_mpc_step_side", "dragg_mpc_aggregate_rows"]
+           "dragg_mpc_lag_reset", "dragg_mpc_step_main", "dragg_mpc_step_side", "dragg_mpc_aggregate_rows",
+           "dragg_mpc_side_workspace_bytes", "dragg_mpc_side_grid", "dragg_mpc_source_hash"]
 
 _LIB = None
 
@@ -110,14 +111,29 @@ class DraggError(RuntimeError):
     pass
 
 
+def check_stamp(path):
+    """The in-tree library must be built from the sources beside it: its source stamp (sha-256 of
+    csrc/ and the header, dragg_amd/build.py) must equal theirs.  A stale library -- sources edited,
+    checked out or copied after the build -- is refused rather than run.  DRAGG_LIB (an experiment's
+    alternative build from other sources) and a tree without the sources are not checked."""
+    from . import build as B
+    if os.environ.get("DRAGG_LIB") or os.path.abspath(path) != os.path.abspath(B.OUT) or not B.sources_present():
+        return
+    got, want = B.stamp_of(path), B.source_hash()
+    if got != want:
+        raise DraggError(f"{path} is stale: built from sources {got}, the sources are now {want}; rebuild it "
+                         "with `python -m dragg_amd.build`")
+
+
 def load(path=LIB_PATH):
-    """Load the HIP library (raises if it was not built)."""
+    """Load the HIP library (raises if it was not built, or was built from other sources)."""
     global _LIB
     if _LIB is not None:
         return _LIB
     if not os.path.exists(path):
         raise DraggError(f"{path} not found: build it with `python -m dragg_amd.build` "
                          "(there is no CPU fallback)")
+    check_stamp(path)
     lib = ctypes.CDLL(path)
     lib.dragg_mpc_abi_version.restype = ctypes.c_int
     lib.dragg_mpc_strerror.restype = ctypes.c_char_p
@@ -125,6 +141,10 @@ def load(path=LIB_PATH):
     lib.dragg_mpc_lds_bytes.argtypes = [ctypes.POINTER(Dims)]
     lib.dragg_mpc_workspace_bytes.argtypes = [ctypes.POINTER(Dims)]
     lib.dragg_mpc_workspace_bytes.restype = ctypes.c_int64
+    lib.dragg_mpc_side_workspace_bytes.argtypes = [ctypes.POINTER(Dims)]
+    lib.dragg_mpc_side_workspace_bytes.restype = ctypes.c_int64
+    lib.dragg_mpc_side_grid.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(ctypes.c_int32)]
+    lib.dragg_mpc_source_hash.restype = ctypes.c_char_p
     lib.dragg_mpc_step.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Problem), ctypes.POINTER(Hash),
                                    ctypes.POINTER(Out), ctypes.c_int32, c_dp, c_dp]
     lib.dragg_mpc_solve_explicit.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Problem),
@@ -143,8 +163,20 @@ def load(path=LIB_PATH):
     lib.dragg_mpc_aggregate_rows.argtypes = [ctypes.POINTER(Dims), c_dp, ctypes.c_int32, c_dp, c_dp]
     if lib.dragg_mpc_abi_version() != ABI_VERSION:
         raise DraggError("ABI version mismatch between dragg_amd and libdragg_mi355x.so")
+    if not os.environ.get("DRAGG_LIB"):
+        from . import build as B
+        if B.sources_present() and lib.dragg_mpc_source_hash().decode() != B.source_hash():
+            raise DraggError(f"{path}: the loaded library's source stamp is not the sources'")
     _LIB = lib
     return lib
+
+
+def side_grid(dims):
+    """The lag mode's side-pass grids (hot, mid, big, step-function) for these dims under the current
+    knobs (DRAGG_SIDE_GRID clamped to each launch's per-block scratch; host-only query)."""
+    g = (ctypes.c_int32 * 4)()
+    check(load().dragg_mpc_side_grid(ctypes.byref(dims), g))
+    return list(g)
 
 
 def reload_knobs():

@@ -60,6 +60,9 @@ class DeviceAggregator:
                      if keep_history else None)
         self.agg_hist = torch.zeros((num_timesteps, 3), dtype=torch.float64, device=dev)
         self.status_hist = torch.zeros((num_timesteps, n), dtype=torch.int32, device=dev)
+        # every solve's int_path bits (dragg_mpc_out.int_path): which solves kept an approximate schedule
+        # (bits 0-11, approx_counts) -- the reference's solve is exact up to GLPK's gap (mpc_calc.py:447-451)
+        self.path_hist = torch.zeros((num_timesteps, n), dtype=torch.int32, device=dev)
         self._deferred = []          # steps whose agg_hist row holds this rank's sums only
         # overlap (lag mode, MPCBatch.enable_lag): a home whose chain needs the slow step-function DP
         # finishes that step on a side stream while the others go on (run_rbo_mpc has no feedback
@@ -77,11 +80,35 @@ class DeviceAggregator:
         t = self.timestep
         hist = self.hist[t] if self.hist is not None else None
         if self.overlap and noise is None:
-            self.batch.step_lagged(t, hist, self.status_hist[t])
+            self.batch.step_lagged(t, hist, self.status_hist[t], path_row=self.path_hist[t])
         else:
             self.batch.step(t, noise=noise, hist=hist)
             self.status_hist[t].copy_(self.batch.status, non_blocking=True)
+            if hasattr(self.batch, "int_path"):
+                self.path_hist[t].copy_(self.batch.int_path, non_blocking=True)
         self.timestep += 1
+
+    def approx_counts(self, lo=0, hi=None):
+        """Solves of steps [lo, hi) (default: all so far) by int_path: {"approx_solves": solves that
+        kept an approximate integer schedule (int_path bits 0-11: reason 3, an RL-priced front past
+        2,048 labels without DRAGG_FLAG_EXACT; reason 6, the step-function DP past its pool or work
+        bound), "step_dp_solves": solves by the exact step-function DP (bit 15), "later_launch_solves":
+        solves finished by the mid / big / step-function launches (bit 12)}, over every rank."""
+        self.drain()
+        hi = self.timestep if hi is None else hi
+        p = self.path_hist[lo:hi]
+        v = torch.stack([((p & L.PATH_APPROX_MASK) != 0).sum(), ((p & L.PATH_STEPS) != 0).sum(),
+                         ((p & L.PATH_SECOND) != 0).sum()]).to(torch.int64)
+        if self.world > 1:
+            torch.distributed.all_reduce(v, group=self.group)
+        a, s, m = (int(x) for x in v.cpu().tolist())
+        return {"approx_solves": a, "step_dp_solves": s, "later_launch_solves": m}
+
+    def approx_solves(self):
+        """[(timestep, global home index, int_path)] of this shard's approximate solves so far."""
+        self.drain()
+        p = self.path_hist[:self.timestep].cpu().numpy()
+        return [(int(t), int(self.index[i]), int(p[t, i])) for t, i in np.argwhere((p & L.PATH_APPROX_MASK) != 0)]
 
     def drain(self):
         """Overlap mode: wait (in stream order) for the side stream, then fill the sums of the steps
@@ -195,6 +222,7 @@ class DeviceAggregator:
                  "vals": self.batch.vals.cpu(), "fc": self.batch.fc.cpu(),
                  "reward_price": self.batch.rp.cpu(),
                  "agg_hist": self.agg_hist[:t].cpu(), "status_hist": self.status_hist[:t].cpu(),
+                 "path_hist": self.path_hist[:t].cpu(),
                  "deferred": torch.as_tensor(self._deferred, dtype=torch.long),
                  "hist": self.hist[:t].cpu() if self.hist is not None else None}
         tmp = path + ".tmp"
@@ -222,6 +250,8 @@ class DeviceAggregator:
         self.batch.set_reward_price(st["reward_price"].to(self.device))
         self.agg_hist[:t].copy_(st["agg_hist"])
         self.status_hist[:t].copy_(st["status_hist"])
+        if st.get("path_hist") is not None:
+            self.path_hist[:t].copy_(st["path_hist"])
         self._deferred = st["deferred"].tolist()
         if self.hist is not None and st["hist"] is not None:
             self.hist[:t].copy_(st["hist"])

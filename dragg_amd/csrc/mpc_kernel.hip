@@ -24,6 +24,15 @@
 
 #define DEV static __device__ __forceinline__
 
+// sha-256 of this file and the header, stamped by dragg_amd/build.py (-DDRAGG_SOURCE_HASH): the host
+// refuses a library whose stamp differs from the sources beside it (dragg_amd/_lib.py); the prefix lets
+// the build find the stamp in the .so without loading it
+#ifndef DRAGG_SOURCE_HASH
+#define DRAGG_SOURCE_HASH "unstamped"
+#endif
+#define kSourcePrefix "dragg-source-sha256:"
+static const char kSourceStamp[] = kSourcePrefix DRAGG_SOURCE_HASH;
+
 namespace {
 
 constexpr int NS = 8;        // variable slots per stage
@@ -1488,16 +1497,14 @@ __host__ __device__ inline size_t par_region_bytes(int N, int H) {
     return ((size_t)N * H * NB_CAP * sizeof(uint16_t) + 255) / 256 * 256;
 }
 // then [N][8H] f64 solutions, the list of homes the hot launch defers to the second one
-// ([N] i32 + its length), (256-aligned) the front DP's LP cost-to-go rows [N][H + 1][64] (x, v),
-// and (256-aligned) the second launch's back-pointer rows [SECOND_SLOTS][H][NF_BIG] u16, one
-// block of that persistent launch per slot
+// ([N] i32 + its length) and (256-aligned) the second launch's back-pointer rows
+// [SECOND_SLOTS][H][NF_BIG] u16, one block of that persistent launch per slot.  From the deferred
+// list to the end of the mid launch's rows (below) the workspace holds only lists and per-block
+// scratch: that span is all the lag mode's side workspace needs (side_workspace_bytes); the per-home
+// regions (back-pointers, solutions, LP rows, cell rows) come before or after it.
 __host__ __device__ inline size_t defer_offset(int N, int H) { return par_region_bytes(N, H) + (size_t)N * 8 * H * 8; }
-__host__ __device__ inline size_t w_region_offset(int N, int H) {
-    return (defer_offset(N, H) + (size_t)(N + 2) * sizeof(int) + 255) / 256 * 256;
-}
-__host__ __device__ inline size_t w_region_bytes(int N, int H) { return (size_t)N * (H + 1) * 64 * 16; }
 __host__ __device__ inline size_t big_region_offset(int N, int H) {
-    return (w_region_offset(N, H) + w_region_bytes(N, H) + 255) / 256 * 256;
+    return (defer_offset(N, H) + (size_t)(N + 2) * sizeof(int) + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t big_region_bytes(int H) { return (size_t)SECOND_SLOTS * H * NF_BIG * sizeof(uint16_t); }
 // then the list of homes the second launch hands to DM_NARROW ([N] i32 + its length) and
@@ -1523,10 +1530,17 @@ __host__ __device__ inline size_t mid_list_offset(int N, int H) {
 __host__ __device__ inline size_t mid_region_offset(int N, int H) {
     return (mid_list_offset(N, H) + (size_t)(N + 2) * sizeof(int) + 255) / 256 * 256;
 }
+// then (256-aligned) the front DP's LP cost-to-go rows [N][H + 1][64] (x, v), per home
+__host__ __device__ inline size_t w_region_offset(int N, int H) {
+    return (mid_region_offset(N, H) + (size_t)MID_SLOTS_MAX * H * NF_MID * sizeof(uint16_t) + 255) / 256 * 256;
+}
+__host__ __device__ inline size_t w_region_bytes(int N, int H) { return (size_t)N * (H + 1) * 64 * 16; }
+// the lag mode's side workspace: the lists and per-block scratch [defer_offset, w_region_offset)
+__host__ __device__ inline size_t side_workspace_bytes(int N, int H) { return w_region_offset(N, H) - defer_offset(N, H); }
 // then (256-aligned), with a reward-price list (dims.n_rp > 1: RL prices possible), the cell bound's
 // rows of every home's indoor-air chain [N][H + 1][NCELL] f32 (cell_kernel; row 0, cell 0: 1 = valid)
 __host__ __device__ inline size_t cell_region_offset(int N, int H) {
-    return (mid_region_offset(N, H) + (size_t)MID_SLOTS_MAX * H * NF_MID * sizeof(uint16_t) + 255) / 256 * 256;
+    return (w_region_offset(N, H) + w_region_bytes(N, H) + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t cell_region_bytes(int N, int H, bool cells) {
     return cells ? (size_t)N * (H + 1) * NCELL * sizeof(float) : 0;
@@ -4219,6 +4233,10 @@ constexpr int HOME_MASK = 0x0FFFFFFF;
 constexpr int BK_OK = 1 << 28;           // the bucketed DP found a schedule (in the solution rows)
 constexpr int BK_DONE = 1 << 29;         // the bucketed DP already ran for the deferred chain (mid -> big)
 constexpr int BK_BEAM = (int)(1u << 31); // ... and that schedule is the beam pass's (diagnostic: int_path bit 17)
+// step-function list entries (bit 31, the big list's BK_BEAM): a chain the hot launch handed straight over
+// (a feasible set narrower than one duty step, dp_front -2), whose bucketed DP -- the upper bound of the
+// step-function DP and its capacity escape's schedule -- the step-function launch runs itself
+constexpr int BK_NEED = (int)(1u << 31);
 
 template <bool EXPLICIT, int MODE, int NW = 1, int ILP = 1>
 DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int first_chain, int eflags = 0) {
@@ -4356,6 +4374,13 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 // an upper bound on the chain's optimum: the bucketed schedule the mid / big launch left in the
                 // solution rows; without one the feasibility pass (all duty costs 0: the feasible set as a few
                 // intervals, microseconds) decides whether any schedule exists and gives one
+                if (chain == first_chain && (eflags & BK_NEED)) {
+                    // the bucketed schedule of a chain the hot launch handed over (what the mid launch computes
+                    // for the chains it hands over), here on all NT threads (dp_thermal is bit-identical for any
+                    // thread count)
+                    const bool okb = dp_thermal<6>(h, D, lane, NT, g, x0, lo0, hi0, lo, hi, sx, sv);
+                    eflags = BK_DONE | (okb ? BK_OK : 0);
+                }
                 double ub = (chain == first_chain && (eflags & BK_OK)) ? sched_cost() : INFINITY;
                 // the bucketed schedule (x, u per stage) kept aside in the chain's battery slots (zero until
                 // the battery LP, which runs after both chains): what stands in if the DP runs out of room
@@ -4484,8 +4509,16 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
             }
             if (r >= 0) {
                 ok = r == 1;
-            } else if (MODE == DM_FRONT) {                 // leave the home to DM_BUCKET
-                if (lane == 0) list[atomicAdd(list + N, 1)] = home | (chain << 30);
+            } else if (MODE == DM_FRONT) {                 // leave the home to a later launch
+                // a feasible set narrower than one duty step (-2): no front DP takes the chain (the mid launch's
+                // would return -2 again) and the exact step-function DP solves it; the mid launch would only run
+                // the bucketed DP for that DP's bound, so the chain goes straight to the step-function launch,
+                // which runs the bucketed DP itself (BK_NEED): one launch fewer on the chain's path (lag mode:
+                // a lagging home's side pass is hot + step-function, not hot + mid + step-function)
+                if (lane == 0) {
+                    if (r == -2 && h.S == 6) nlist[atomicAdd(nlist + N, 1)] = home | (chain << 30) | BK_NEED;
+                    else list[atomicAdd(list + N, 1)] = home | (chain << 30);
+                }
                 return;
             } else {
                 pf.mark(DRAGG_PH_INTEGER);
@@ -5030,6 +5063,15 @@ constexpr int SIDE_HOT_BLOCKS = 16;         // persistent blocks of the side pas
 constexpr int SIDE_MID_BLOCKS = 16;         // ... mid launch
 constexpr int SIDE_BIG_BLOCKS = 16;         // ... big launch
 constexpr int SIDE_NARROW_BLOCKS = 2;       // ... step-function launch (each needs a whole CU's LDS)
+// blocks of one side-pass launch: the DRAGG_SIDE_GRID entry (knob > 0) or the default, at most one per home
+// and at most `slots` (the launch's per-block scratch regions), at least one
+int side_grid_blocks(int knob, int dflt, int N, int slots) { return max(1, min(min(N, slots), knob > 0 ? knob : dflt)); }
+void side_grids(int N, int out[4]) {
+    const int* sg = knobs().side_grid;
+    const int cap[4] = {N, MID_SLOTS_MAX, SECOND_SLOTS, narrow_slots(N)};
+    const int dflt[4] = {SIDE_HOT_BLOCKS, SIDE_MID_BLOCKS, SIDE_BIG_BLOCKS, SIDE_NARROW_BLOCKS};
+    for (int i = 0; i < 4; ++i) out[i] = side_grid_blocks(sg[i], dflt[i], N, cap[i]);
+}
 int launch_lag(const KArgs& a, bool side, hipStream_t s) {
     static int attr_dev[MAX_DEV][10] = {};
     int dev = 0;
@@ -5041,7 +5083,10 @@ int launch_lag(const KArgs& a, bool side, hipStream_t s) {
     int* const len = reinterpret_cast<int*>(lw + defer_offset(N, H)) + N;
     int* const blen = reinterpret_cast<int*>(lw + mid_list_offset(N, H)) + N;
     KArgs b = a;
-    b.force_steps = 0;
+    // DRAGG_FORCE_STEP_DP holds here too: the hot launches list every home's chains in the step's narrow
+    // list (lag->narrow), which the side pass's step-function launch then solves.  (DRAGG_WAVES_PER_HOME
+    // does not: both passes run the one-wave hot kernel; the header says so.)
+    b.force_steps = knobs().force_steps;
     b.step_pool_cap = knobs().step_pool_cap;
     b.step_work_cap = knobs().step_work_cap;
     const size_t lds = kernel_lds_bytes(&a.d);
@@ -5067,19 +5112,21 @@ int launch_lag(const KArgs& a, bool side, hipStream_t s) {
     b.hot_list = a.skip;
     b.skip = nullptr;
     b.side = 1;
-    const int* sg = knobs().side_grid;
-    auto grid = [&](int i, int dflt) { return max(1, min(N, sg[i] > 0 ? sg[i] : dflt)); };
-    int rc = launch_kernel(side_front_kernel, attr[0], b, grid(0, SIDE_HOT_BLOCKS), WAVE, lds, s);
+    // the persistent launches index per-block scratch by blockIdx.x: a DRAGG_SIDE_GRID entry is clamped to
+    // its region's slots (the mid launch's MID_SLOTS_MAX rows, the big launch's SECOND_SLOTS, the
+    // step-function launch's narrow_slots(N) pools; the hot and cell launches keep no per-block scratch)
+    int grid[4];
+    side_grids(N, grid);
+    int rc = launch_kernel(side_front_kernel, attr[0], b, grid[0], WAVE, lds, s);
     b.hot_list = nullptr;
     if (!rc && a.d.n_rp > 1)
-        rc = launch_kernel(cell_kernel, attr[7], b, grid(1, SIDE_MID_BLOCKS), NT_CELL, (size_t)cell_lds_bytes(H), s);
-    if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_MID, NW_MID>, attr[6], b,
-                                grid(1, SIDE_MID_BLOCKS), NW_MID * WAVE,
+        rc = launch_kernel(cell_kernel, attr[7], b, grid[1], NT_CELL, (size_t)cell_lds_bytes(H), s);
+    if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_MID, NW_MID>, attr[6], b, grid[1], NW_MID * WAVE,
                                 (size_t)mid_layout(H, a.d.sub_steps).bytes, s);
-    if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_BUCKET, NW_BIG>, attr[2], b, grid(2, SIDE_BIG_BLOCKS),
+    if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_BUCKET, NW_BIG>, attr[2], b, grid[2],
                                 NW_BIG * WAVE, (size_t)big_layout(H, a.d.sub_steps).bytes, s);
     if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_NARROW, NT_STEPS / WAVE>, attr[5], b,
-                                grid(3, SIDE_NARROW_BLOCKS), NT_STEPS, (size_t)narrow_layout(H, a.d.sub_steps).bytes, s);
+                                grid[3], NT_STEPS, (size_t)narrow_layout(H, a.d.sub_steps).bytes, s);
     return rc;
 }
 
@@ -5105,6 +5152,24 @@ int64_t dragg_mpc_workspace_bytes(const dragg_mpc_dims* dims) {
     if (rc) return rc;
     return (int64_t)workspace_bytes(dims);
 }
+
+int64_t dragg_mpc_side_workspace_bytes(const dragg_mpc_dims* dims) {
+    const int rc = check_dims(dims);
+    if (rc) return rc;
+    return direct_mode(dims) ? (int64_t)side_workspace_bytes(dims->n_homes, dims->horizon) : 0;
+}
+
+int dragg_mpc_side_grid(const dragg_mpc_dims* dims, int32_t* grid4) {
+    const int rc = check_dims(dims);
+    if (rc) return rc;
+    if (!grid4) return DRAGG_E_ARG;
+    int g[4];
+    side_grids(dims->n_homes, g);
+    for (int i = 0; i < 4; ++i) grid4[i] = dims->n_homes > 0 ? g[i] : 0;
+    return DRAGG_OK;
+}
+
+const char* dragg_mpc_source_hash(void) { return kSourceStamp + sizeof(kSourcePrefix) - 1; }
 
 int dragg_mpc_lds_bytes(const dragg_mpc_dims* dims) {
     const int rc = check_dims(dims);
@@ -5147,7 +5212,11 @@ static int lag_args(const dragg_mpc_dims* dims, const dragg_mpc_problem* prob, d
     *a = KArgs{};
     a->d = *dims; a->p = *prob; a->vals = hash->vals; a->fc = hash->fc; a->out = *out; a->noise = nullptr;
     a->t = timestep;
-    a->lws = reinterpret_cast<char*>(side ? lag->side_workspace : prob->workspace);
+    // the side workspace holds only the span [defer_offset, w_region_offset) of the layout: its base stands
+    // at defer_offset (the kernels address lists and per-block scratch as lws + their layout offset, all
+    // inside that span; nothing below defer_offset is addressed through lws)
+    a->lws = side ? reinterpret_cast<char*>(lag->side_workspace) - defer_offset(dims->n_homes, dims->horizon)
+                  : reinterpret_cast<char*>(prob->workspace);
     a->clk = lag->clock; a->skip = lag->skipped; a->nar = lag->narrow;
     return DRAGG_OK;
 }

@@ -147,10 +147,15 @@ def _draw_profiles(path, n_homes, ndays, tank_size):
     nr, nc = wd.shape
     z = np.random.randn(nc * nr).reshape(nc, nr).T
     wd = pd.DataFrame(wd.to_numpy() * (1 + 0.2 * z), index=wd.index, columns=wd.columns)
-    wd = wd.resample("h").sum()
+    hourly = wd.resample("h").sum().to_numpy()
     out = []
+    nc_ = hourly.shape[1]
     for j in range(n_homes):
-        prof = wd.sample(axis="columns").values.reshape(-1, 24)
+        # `wd.sample(axis="columns")` is np.random.choice(columns, size=1, replace=False) on the global
+        # legacy stream (pandas' sample with random_state=None), then that column: the same draw here,
+        # without the 10^4 DataFrame copies
+        col = np.random.choice(nc_, size=1, replace=False)
+        prof = hourly[:, col].reshape(-1, 24)
         days = prof[np.random.choice(prof.shape[0], ndays)].flatten()
         out.append(np.clip(days, 0, tank_size[j]).tolist())
     return out

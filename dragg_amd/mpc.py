@@ -160,6 +160,10 @@ class MPCBatch:
 
     # ------------------------------------------------------------------ environment
     def set_environment(self, oat, ghi, tou, start_index):
+        # (lag mode: a side pass still in flight holds raw pointers to the current lists, and their blocks
+        # belong to the main stream's allocator pool: join it before they can be freed and reused)
+        if getattr(self, "lag", None) is not None:
+            self.drain()
         dev = self.device
         self.oat = torch.tensor(np.asarray(oat, dtype=float), dtype=torch.float64, device=dev)
         self.ghi = torch.tensor(np.asarray(ghi, dtype=float), dtype=torch.float64, device=dev)
@@ -180,6 +184,8 @@ class MPCBatch:
             # np.array(rp[:H]) + tou[:H] raises in the reference (mpc_calc.py:353)
             raise ValueError(f"operands could not be broadcast together: reward_price has {n} "
                              f"entries, horizon is {self.H}")
+        if getattr(self, "lag", None) is not None:
+            self.drain()                     # (as in set_environment: the side pass reads self.rp)
         self.rp = rp if torch.is_tensor(rp) else torch.tensor(rp, dtype=torch.float64, device=self.device)
         self.dims.n_rp = n
         if self.workspace is not None or hasattr(self, "vals"):
@@ -197,7 +203,15 @@ class MPCBatch:
             self.drain()
             self.workspace = torch.empty(need, dtype=torch.int64, device=self.device)
             if self.lag is not None:
-                self.lag["side_ws"] = torch.empty_like(self.workspace)
+                self.lag["side_ws"] = self._side_workspace()
+
+    def _side_workspace(self):
+        """The lag mode's side workspace: only the lists and per-block scratch of the side pass
+        (dragg_mpc_side_workspace_bytes; the per-home regions stay in self.workspace)."""
+        sb = self.lib.dragg_mpc_side_workspace_bytes(ctypes.byref(self.dims))
+        if sb < 0:
+            L.check(int(sb))
+        return torch.empty(max(1, (sb + 7) // 8), dtype=torch.int64, device=self.device)
 
     # ------------------------------------------------------------------ structs
     def _problem(self):
@@ -243,7 +257,7 @@ class MPCBatch:
                 "ring": int(ring),
                 "lists": torch.zeros((ring, 2, L.lag_list_ints(self.N)), dtype=torch.int32, device=dev),
                 "clock": torch.zeros(max(1, self.N), dtype=torch.int32, device=dev),
-                "side_ws": torch.empty_like(self.workspace) if self.workspace is not None else None,
+                "side_ws": self._side_workspace() if self.workspace is not None else None,
                 "stream": torch.cuda.Stream(device=dev),
                 "main_done": torch.cuda.Event(),
                 "side_done": [torch.cuda.Event() for _ in range(ring)],
@@ -252,15 +266,16 @@ class MPCBatch:
                 "pending": False,               # side work not yet joined into the main stream
             }
 
-    def step_lagged(self, t, hist, status_row, stream=None):
+    def step_lagged(self, t, hist, status_row, stream=None, path_row=None):
         """One timestep in lag mode: the main pass on `stream` (default: the current one), the side pass
-        on the side stream after it.  `hist` ([NVAL][N]) and `status_row` ([N] int32) receive the step's
-        per-home results -- a lagging home's later -- so they must be this step's own rows; nothing of
-        the step may be read before drain()."""
+        on the side stream after it.  `hist` ([NVAL][N]), `status_row` ([N] int32) and `path_row` ([N]
+        int32, the int_path bits; default self.int_path) receive the step's per-home results -- a
+        lagging home's later -- so they must be this step's own rows; nothing of the step may be read
+        before drain()."""
         with torch.cuda.device(self.device):
-            return self._step_lagged(t, hist, status_row, stream)
+            return self._step_lagged(t, hist, status_row, stream, path_row)
 
-    def _step_lagged(self, t, hist, status_row, stream):
+    def _step_lagged(self, t, hist, status_row, stream, path_row=None):
         lg = self.lag
         if lg is None:
             raise RuntimeError("enable_lag() first")
@@ -279,7 +294,8 @@ class MPCBatch:
             main.wait_event(lg["side_done"][slot])      # the side pass of step t - ring is done with the lists
         prob, hsh = self._problem(), self._hash()
         out = L.Out(status=L.ptr(status_row), iters=L.ptr(self.iters), obj=L.ptr(self.obj),
-                    relax_obj=L.ptr(self.relax_obj), hist=L.ptr(hist), cycles=None, int_path=L.ptr(self.int_path))
+                    relax_obj=L.ptr(self.relax_obj), hist=L.ptr(hist), cycles=None,
+                    int_path=L.ptr(path_row if path_row is not None else self.int_path))
         L.check(self.lib.dragg_mpc_step_main(ctypes.byref(self.dims), ctypes.byref(prob), ctypes.byref(hsh),
                                              ctypes.byref(out), int(t), ctypes.byref(lag), L.stream_ptr(main, self.device)))
         lg["main_done"].record(main)
@@ -291,7 +307,7 @@ class MPCBatch:
         lg["last"] = slot
         lg["next"] = t + 1
         lg["pending"] = True
-        self._keep = (hist, status_row)
+        self._keep = (hist, status_row, path_row)
 
     def drain(self, stream=None):
         """Join the side stream into `stream` (default: the current one): after this, everything the

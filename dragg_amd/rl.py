@@ -65,8 +65,9 @@ class SetpointAgent:
 
 
 def agent_policy(aggregator):
-    """The policy a `run_rl_agg = true` config runs with: `SetpointAgent`, its gain from
-    `rl.parameters.learning_rate` when given (README.md:58-63)."""
-    p = aggregator.config.get("rl", {}).get("parameters", {})
-    kp = float(p.get("learning_rate", 1.0)) if p else 1.0
-    return SetpointAgent(aggregator.config, kp=kp).act
+    """The policy a `run_rl_agg = true` config runs with: `SetpointAgent`, its gains from the keys of
+    its own, `rl.parameters.kp` (default 1.0) and `rl.parameters.ki` (default 0.1).  The reference's
+    `rl.parameters.learning_rate` (README.md:58-63) is a learning agent's step size, not a controller
+    gain: it is left to an agent wrapped by `policy_from_agent`."""
+    p = aggregator.config.get("rl", {}).get("parameters", {}) or {}
+    return SetpointAgent(aggregator.config, kp=float(p.get("kp", 1.0)), ki=float(p.get("ki", 0.1))).act

@@ -23,6 +23,9 @@ raise.
 """
 import json
 import os
+import time
+import warnings
+from contextlib import contextmanager
 from datetime import datetime
 
 import numpy as np
@@ -34,6 +37,20 @@ from . import results as R
 class Aggregator:
     def __init__(self, data_dir=None, config_file=None, outputs_dir="outputs", int_mode="round", device=None,
                  group=None, first_name=None, batch_cls=None):
+        # wall seconds per phase of the run (tools/e2e.py): {phase: seconds}, accumulated
+        self.timings = {}
+        with self._phase("config_and_weather"):
+            self._init(data_dir, config_file, outputs_dir, int_mode, device, group, first_name, batch_cls)
+
+    @contextmanager
+    def _phase(self, name):
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            self.timings[name] = self.timings.get(name, 0.0) + time.perf_counter() - t0
+
+    def _init(self, data_dir, config_file, outputs_dir, int_mode, device, group, first_name, batch_cls):
         env = os.environ
         self.data_dir = os.path.expanduser(env.get("DATA_DIR", "data")) if data_dir is None else data_dir
         self.outputs_dir = outputs_dir
@@ -81,15 +98,17 @@ class Aggregator:
     def get_homes(self):
         n = self.config["community"]["total_number_homes"]
         path = os.path.join(self.outputs_dir, f"all_homes-{n}-config.json")
-        if not self.config["community"]["overwrite_existing"] and os.path.isfile(path):
-            with open(path) as f:
-                self.all_homes = json.load(f)
-        else:
-            draws = os.path.join(self.data_dir, self.config["home"]["wh"]["waterdraw_file"])
-            self.all_homes = I.create_homes(self.config, self.num_timesteps, self.dt, draws, self.first_name)
-        I.check_home_counts(self.all_homes, self.config)
+        with self._phase("create_homes"):
+            if not self.config["community"]["overwrite_existing"] and os.path.isfile(path):
+                with open(path) as f:
+                    self.all_homes = json.load(f)
+            else:
+                draws = os.path.join(self.data_dir, self.config["home"]["wh"]["waterdraw_file"])
+                self.all_homes = I.create_homes(self.config, self.num_timesteps, self.dt, draws, self.first_name)
+            I.check_home_counts(self.all_homes, self.config)
         if self.rank == 0:
-            R.write_home_configs(self.outputs_dir, self.all_homes, n)
+            with self._phase("write_home_configs"):
+                R.write_home_configs(self.outputs_dir, self.all_homes, n)
         self.max_poss_load = sum(I.max_load(h) for h in self.all_homes)
 
     def _device_community(self):
@@ -124,27 +143,58 @@ class Aggregator:
         them apart): they check that together and all raise otherwise.  `stop_after`: return
         after the first checkpoint at or past that many steps (an interrupted run)."""
         self.start_time = datetime.now()
-        self._device_community()
+        with self._phase("upload"):
+            self._device_community()
+            self._sync()
         t0 = 0
         if resume:                                 # every rank loads, then all agree (or all raise)
             t0 = self.dev.resume(self.state_path())
             self.timestep = t0
+        loop_t0 = time.perf_counter()
+        ckpt = self.timings.get("checkpoints", 0.0)
         for t in range(t0, self.num_timesteps):
             noise = noise_fn(t)[:, self.dev.index] if noise_fn is not None else None
             self.dev.run_iteration(noise)
             self.dev.collect_data(defer=True)      # no feedback: the sums are reduced at the end
             self.timestep = t + 1
             if (t + 1) % self.checkpoint_interval == 0:
-                # the reference raises inside the step that fails (mpc_calc.py:280-289,
-                # 537-539); checking at each checkpoint (one host sync) keeps post-error data
-                # out of every results.json written
-                self.dev.check_errors()
-                self.write_outputs()
-                self.dev.save_state(self.state_path())
+                with self._phase("checkpoints"):
+                    # the reference raises inside the step that fails (mpc_calc.py:280-289,
+                    # 537-539); checking at each checkpoint (one host sync) keeps post-error data
+                    # out of every results.json written
+                    self.dev.check_errors()
+                    self.write_outputs()
+                    self.dev.save_state(self.state_path())
                 if stop_after is not None and t + 1 >= stop_after:
                     return                         # an interrupted run
         self.dev.reduce_history()
         self.dev.check_errors()
+        self.check_solve_paths()
+        # the step loop: launches and device time of every step, without the checkpoint writes
+        self.timings["step_loop"] = (self.timings.get("step_loop", 0.0) + time.perf_counter() - loop_t0
+                                     - (self.timings.get("checkpoints", 0.0) - ckpt))
+
+    def _sync(self):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+        except ImportError:
+            pass
+
+    def check_solve_paths(self):
+        """The run's solve-path counts over every rank (`self.solve_paths`: approximate solves, solves by
+        the step-function DP, solves finished by a later launch); warns when a solve kept an approximate
+        integer schedule -- the reference's GLPK_MI solve is exact up to its gap (mpc_calc.py:447-451),
+        so such a run is not the reference's to that tolerance (int_path reasons 3 and 6)."""
+        self.solve_paths = self.dev.approx_counts()
+        n = self.solve_paths["approx_solves"]
+        if n:
+            where = self.dev.approx_solves()[:5]
+            warnings.warn(f"{n} solve(s) kept an approximate integer schedule (int_path reason 3 / 6; first on "
+                          f"this rank as (timestep, home, int_path): {where}); rerun with a larger "
+                          "DRAGG_STEP_WORK_CAP / DRAGG_STEP_POOL_CAP or dims.flags DRAGG_FLAG_EXACT", RuntimeWarning)
+        return self.solve_paths
 
     # ------------------------------------------------------------------ RL aggregator (§8 F4)
     # aggregator.py:677-696
@@ -262,6 +312,7 @@ class Aggregator:
                 self.dev.check_errors()
                 self.write_outputs()
         self.dev.check_errors()
+        self.check_solve_paths()
         return self.write_outputs()
 
     def _history(self):
@@ -307,24 +358,39 @@ class Aggregator:
 
     # aggregator.py:783-844 (summarize_baseline + write_outputs)
     def write_outputs(self):
-        hist = self._history()
+        with self._phase("history_gather"):
+            hist = self._history()
         if self.rank != 0:
             return None
         t_diff = datetime.now() - self.start_time
-        collected = R.new_collected(self.all_homes)
-        R.append_history(collected, self.checked, hist)
-        # the RL case's list starts with setup_rl_agg_run's 0 (aggregator.py:887)
-        loads = self.baseline_agg_load_list if "rl" in self.case else R.aggregate_loads(hist)
-        self.max_agg_load = max(loads)
-        self.max_agg_load_list.append(self.max_agg_load)
-        collected["Summary"] = R.summary(
-            self.case, self.start_dt, self.end_dt, t_diff.total_seconds(),
-            self.config["home"]["hems"]["prediction_horizon"], self.config["community"]["total_number_homes"],
-            loads, self.all_data.loc[self.mask, "OAT"].values.tolist(),
-            self.all_data.loc[self.mask, "GHI"].values.tolist(), self.all_rps.tolist(), self.all_sps.tolist(),
-            tou=self.all_data.loc[self.mask, "tou"].values.tolist())
-        self.collected_data = collected
-        return R.write_results(self.run_dir, self.case, collected)
+        with self._phase("results_build"):
+            # the RL case's list starts with setup_rl_agg_run's 0 (aggregator.py:887)
+            loads = self.baseline_agg_load_list if "rl" in self.case else R.aggregate_loads(hist)
+            self.max_agg_load = max(loads)
+            self.max_agg_load_list.append(self.max_agg_load)
+            summary = R.summary(
+                self.case, self.start_dt, self.end_dt, t_diff.total_seconds(),
+                self.config["home"]["hems"]["prediction_horizon"], self.config["community"]["total_number_homes"],
+                loads, self.all_data.loc[self.mask, "OAT"].values.tolist(),
+                self.all_data.loc[self.mask, "GHI"].values.tolist(), self.all_rps.tolist(), self.all_sps.tolist(),
+                tou=self.all_data.loc[self.mask, "tou"].values.tolist())
+            # the reference's collected_data dict (aggregator.py:589-615, 737-748) is built when read
+            self._collected_src = (self.all_homes, self.checked, hist, summary)
+            self._collected = None
+        with self._phase("results_write"):
+            # the same bytes as json.dump(collected_data, indent=4), straight from the history array
+            return R.write_results_history(self.run_dir, self.case, self.all_homes, self.checked, hist, summary)
+
+    @property
+    def collected_data(self):
+        """The reference's `collected_data` (per-home series + "Summary"), as of the last write_outputs."""
+        if getattr(self, "_collected", None) is None and getattr(self, "_collected_src", None) is not None:
+            homes, checked, hist, summary = self._collected_src
+            c = R.new_collected(homes)
+            R.append_history(c, checked, hist)
+            c["Summary"] = summary
+            self._collected = c
+        return getattr(self, "_collected", None)
 
     # aggregator.py:941-970
     def run(self, noise_fn=None, resume=False, stop_after=None):
@@ -337,7 +403,8 @@ class Aggregator:
                                  self.dt_interval, hems["sub_subhourly_steps"], hems["solver"], self.version)
         if sim["run_rbo_mpc"]:
             self.case = "baseline"
-            self.flush()
+            with self._phase("flush"):
+                self.flush()
             self.get_homes()
             self.run_baseline(noise_fn, resume=resume, stop_after=stop_after)
             if stop_after is not None and self.timestep < self.num_timesteps:

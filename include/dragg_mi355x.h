@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DRAGG_MPC_ABI_VERSION 8
+#define DRAGG_MPC_ABI_VERSION 9
 
 /* home types (aggregator.py:425, 468, 520, 555); bit 0 = pv, bit 1 = battery */
 enum dragg_home_type {
@@ -249,6 +249,15 @@ int dragg_mpc_lds_bytes(const dragg_mpc_dims* dims);
 /* Device workspace bytes a launch with these dims needs (problem.workspace); < 0 on error. */
 int64_t dragg_mpc_workspace_bytes(const dragg_mpc_dims* dims);
 
+/* Device bytes of the lag mode's side workspace (dragg_mpc_lag.side_workspace; since v9): the side
+   pass keeps only its device lists and per-block scratch there (the per-home regions are read from
+   problem.workspace), ~0.5 GB at 10k homes, H = 48, against the workspace's 1.34 GB. */
+int64_t dragg_mpc_side_workspace_bytes(const dragg_mpc_dims* dims);
+
+/* The sha-256 of the sources this library was built from (the kernel file and this header; since
+   v9): the host refuses a library whose stamp is not its sources' (a stale build). */
+const char* dragg_mpc_source_hash(void);
+
 /* One closed-loop timestep for all N homes: reads the hash arrays (t > 0) or the
    parameters (t == 0), solves, and writes the hash arrays back in place.
    noise: [H][N] standard normals for the season draw (mpc_calc.py:222) or NULL for the
@@ -270,8 +279,14 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
    DRAGG_STEP_WORK_CAP=n (a smaller pool / work bound of that DP; tests of its capacity path),
    DRAGG_HOT_ILP=1|2 (64-child chunks per front-DP pass of the one-wave hot launch; default: 2 at <= 8 homes
    per CU, else 1; results bit-identical), DRAGG_SIDE_GRID=hot,mid,big,narrow (the lag mode's side-pass
-   grids).  Unset: the defaults. */
+   grids, each clamped to 1 .. its launch's per-block scratch slots: dragg_mpc_side_grid reports the
+   grids in effect).  Unset: the defaults.  Lag mode (dragg_mpc_step_main / _side) honours every knob
+   but DRAGG_WAVES_PER_HOME: both its passes run the one-wave hot kernel. */
 void dragg_mpc_reload_knobs(void);
+
+/* The lag mode's side-pass grids for these dims under the current knobs: grid4 = blocks of its hot,
+   mid (and cell), big and step-function launches (zeros for an empty shard).  Host-only query. */
+int dragg_mpc_side_grid(const dragg_mpc_dims* dims, int32_t* grid4);
 
 /* Fill `info` for these dims (needs a GPU: queries the current device). */
 int dragg_mpc_kernel_info_get(const dragg_mpc_dims* dims, dragg_mpc_kernel_info* info);
@@ -305,7 +320,7 @@ typedef struct dragg_mpc_lag {
     int32_t* clock;             /* [N] timesteps completed per home (dragg_mpc_lag_reset) */
     int32_t* skipped;           /* [DRAGG_LAG_LIST_INTS(N)] the step's homes left to the side pass */
     int32_t* narrow;            /* [DRAGG_LAG_LIST_INTS(N)] the step's step-function DP chains   */
-    void* side_workspace;       /* dragg_mpc_workspace_bytes(dims) bytes, the side pass's own     */
+    void* side_workspace;       /* dragg_mpc_side_workspace_bytes(dims) bytes, the side pass's own */
 } dragg_mpc_lag;
 #define DRAGG_LAG_LIST_INTS(n) ((n) + 4)
 

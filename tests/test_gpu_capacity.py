@@ -43,7 +43,8 @@ def _step_with(agg, snap, env):
         torch.cuda.synchronize()
         b = agg.batch
         return (int(b.status[HOME]), float(b.obj[HOME]), int(b.int_path[HOME]),
-                b.fc[:, :, HOME].cpu().numpy().copy(), b.params[:, HOME].cpu().numpy())
+                b.fc[:, :, HOME].cpu().numpy().copy(), b.params[:, HOME].cpu().numpy(),
+                agg.approx_counts(STEP, STEP + 1)["approx_solves"])
     finally:
         for k, v in old.items():
             if v is None:
@@ -56,11 +57,13 @@ def _step_with(agg, snap, env):
 @pytest.mark.parametrize("env", [{"DRAGG_STEP_POOL_CAP": "64"}, {"DRAGG_STEP_WORK_CAP": "1"}])
 def test_capacity_path_keeps_the_bucketed_schedule_flagged(at_step, env, gpu):
     agg, snap = at_step
-    st0, obj0, path0, _, _ = _step_with(agg, snap, {})
+    st0, obj0, path0, _, _, n0 = _step_with(agg, snap, {})
     assert st0 == L.ST_OPTIMAL and path0 & L.PATH_STEPS and not path0 & L.PATH_APPROX_MASK   # exact by default
-    st, obj, path, fc, par = _step_with(agg, snap, env)
+    assert n0 == 0                                                # the step's solves: none approximate
+    st, obj, path, fc, par, n = _step_with(agg, snap, env)
     assert st == L.ST_OPTIMAL and path & L.PATH_STEPS
     assert path & 2 and (path >> 8) & 0xF == 6, hex(path)       # the tank chain: approximate, reason 6
+    assert n == 1                                                 # ... and counted (DeviceAggregator.approx_counts)
     assert obj >= obj0 - 1e-9 * max(1.0, abs(obj0))               # never below the exact optimum
     assert obj <= obj0 + 0.25 * abs(obj0) + 1e-6                  # the bucketed schedule, not an arbitrary one
     # the kept schedule is feasible: integral duties in [0, S], the tank trajectory inside its box
@@ -71,5 +74,5 @@ def test_capacity_path_keeps_the_bucketed_schedule_flagged(at_step, env, gpu):
     lo, hi = par[L.P["TWMIN"]], par[L.P["TWMAX"]]
     assert np.all(tw[1:H] >= lo - 1e-6) and np.all(tw[1:H] <= hi + 1e-6)
     # a bound of the default size solves the same step exactly again
-    st2, obj2, path2, _, _ = _step_with(agg, snap, {"DRAGG_STEP_POOL_CAP": str(1 << 20)})
+    st2, obj2, path2, _, _, _ = _step_with(agg, snap, {"DRAGG_STEP_POOL_CAP": str(1 << 20)})
     assert (st2, obj2, path2) == (st0, obj0, path0)

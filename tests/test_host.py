@@ -153,22 +153,26 @@ def test_size_queries_without_gpu(lib_path):
     ws = lib.dragg_mpc_workspace_bytes(ctypes.byref(d))
     # u16 back-pointer per front label and stage (NB_CAP = 336), rounded to 256 B, then the
     # [N][8H] f64 stage-slot solutions and the [N] i32 list (+ its length) of the homes deferred to
-    # the second launch, then (256-aligned) the front DP's LP cost-to-go rows [N][H + 1][64] (x, v),
-    # then (256-aligned) the second launch's back-pointer rows [512 blocks][H][NF_BIG = 2048] u16,
-    # then (256-aligned) the [N] i32 list (+ length) of homes for the step-function DP launch and
+    # the second launch, then (256-aligned) the second launch's back-pointer rows [512 blocks][H][NF_BIG =
+    # 2048] u16, then (256-aligned) the [N] i32 list (+ length) of homes for the step-function DP launch and
     # (256-aligned) its storage: min(N, 16) block slots of ([2][2^20] f64 breakpoints / values,
     # [2][8 x 32768] i32 merge ids, [2][256][64] (x, v) LP rows)
     par = (100 * 24 * 336 * 2 + 255) // 256 * 256
-    w_off = (par + 100 * 8 * 24 * 8 + 101 * 4 + 255) // 256 * 256
-    big_off = (w_off + 100 * 25 * 64 * 16 + 255) // 256 * 256
+    defer = par + 100 * 8 * 24 * 8
+    big_off = (defer + 102 * 4 + 255) // 256 * 256
     nl_off = (big_off + 512 * 24 * 2048 * 2 + 255) // 256 * 256
-    nr_off = (nl_off + 101 * 4 + 255) // 256 * 256
+    nr_off = (nl_off + 102 * 4 + 255) // 256 * 256
     # then (256-aligned) the [N] i32 list (+ length) the mid launch hands to the big one and
     # (256-aligned) the mid launch's back-pointer rows [2048 blocks][H][NF_MID = 384] u16
     slot = 2 * 2 ** 20 * 8 + 2 * 8 * 32768 * 4 + 2 * 256 * 64 * 16
     ml_off = (nr_off + 16 * slot + 255) // 256 * 256
-    mr_off = (ml_off + 101 * 4 + 255) // 256 * 256
-    assert ws == mr_off + 2048 * 24 * 384 * 2
+    mr_off = (ml_off + 102 * 4 + 255) // 256 * 256
+    # then (256-aligned) the front DP's LP cost-to-go rows [N][H + 1][64] (x, v)
+    w_off = (mr_off + 2048 * 24 * 384 * 2 + 255) // 256 * 256
+    assert ws == (w_off + 100 * 25 * 64 * 16 + 255) // 256 * 256
+    # the lag mode's side workspace: the lists and per-block scratch only, [defer, w_off)
+    lib.dragg_mpc_side_workspace_bytes.restype = ctypes.c_int64
+    assert lib.dragg_mpc_side_workspace_bytes(ctypes.byref(d)) == w_off - defer
     lds_direct = lib.dragg_mpc_lds_bytes(ctypes.byref(d))
     assert 0 < lds_direct <= 13 * 1024                 # the hot launch: >= 12 homes per CU at H = 24
     d.horizon = 48
@@ -183,6 +187,51 @@ def test_size_queries_without_gpu(lib_path):
     d.horizon = 400                                    # LP kernel's LDS is the binding limit
     d.int_mode = L.INT_RELAX
     assert lib.dragg_mpc_lds_bytes(ctypes.byref(d)) == -4
+
+
+def test_side_grid_clamped_to_scratch_slots(lib_path, monkeypatch):
+    """DRAGG_SIDE_GRID entries are clamped to each side launch's per-block scratch: the
+    step-function launch's narrow_slots(N) = min(N, 16) pools, the big launch's 512 and the mid launch's
+    2,048 rows, and to one block per home."""
+    from dragg_amd import _lib as L
+    d = L.Dims(n_homes=1000, horizon=48, sub_steps=6, dt=4, n_draw_hours=48, n_env=0, n_rp=1,
+               int_mode=L.INT_ROUND, max_iter=0, check_every=0, discount=0.92)
+    try:
+        monkeypatch.delenv("DRAGG_SIDE_GRID", raising=False)
+        L.reload_knobs()
+        assert L.side_grid(d) == [16, 16, 16, 2]
+        monkeypatch.setenv("DRAGG_SIDE_GRID", "5000,4096,9999,32")
+        L.reload_knobs()
+        assert L.side_grid(d) == [1000, 1000, 512, 16]
+        d.n_homes = 3000
+        assert L.side_grid(d) == [3000, 2048, 512, 16]
+        d.n_homes = 5
+        assert L.side_grid(d) == [5, 5, 5, 5]
+        monkeypatch.setenv("DRAGG_SIDE_GRID", "0,-3,1,1")
+        L.reload_knobs()
+        assert L.side_grid(d) == [5, 5, 1, 1]
+    finally:
+        monkeypatch.delenv("DRAGG_SIDE_GRID", raising=False)
+        L.reload_knobs()
+
+
+def test_stale_library_refused(tmp_path, monkeypatch, lib_path):
+    """The library carries its sources' sha-256 (dragg_amd/build.py); the loader refuses one whose stamp
+    is not the sources' beside it."""
+    from dragg_amd import _lib as L, build as B
+    assert B.stamp_of(lib_path) == B.source_hash()
+    assert not B.needs_build()
+    L.check_stamp(lib_path)                           # the fresh build passes
+    assert ctypes.CDLL(lib_path).dragg_mpc_source_hash  # exported
+    stale = tmp_path / "stale.so"
+    data = open(lib_path, "rb").read().replace(B.STAMP_PREFIX + B.source_hash().encode(),
+                                               B.STAMP_PREFIX + b"0" * 64)
+    stale.write_bytes(data)
+    monkeypatch.setattr(B, "OUT", str(stale))
+    monkeypatch.delenv("DRAGG_LIB", raising=False)
+    assert B.needs_build()
+    with pytest.raises(L.DraggError, match="stale"):
+        L.check_stamp(str(stale))
 
 
 def test_solver_name_plug_point():

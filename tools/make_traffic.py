@@ -100,6 +100,10 @@ def main():
     ap.add_argument("--warmup", type=int, required=True)
     ap.add_argument("--rl-price", default="smooth")
     ap.add_argument("--forecast-horizon", type=int, default=1)
+    ap.add_argument("--shard-of", type=int, default=0)
+    ap.add_argument("--shard-rank", default=None, help="the rank of a --shard-of line, or max (--shard-max)")
+    ap.add_argument("--steps-mode", default=None, choices=["lag", "serial", "adaptive"],
+                    help="how the profiled command's steps ran (since round 6; unset: the key of rounds <= 5)")
     ap.add_argument("--command", default="")
     a = ap.parse_args()
     from bench import traffic_key
@@ -107,7 +111,9 @@ def main():
     fh = a.forecast_horizon if rl else 0
     per_unit = 1 + fh
     key = traffic_key(a.homes, a.horizon, a.dt, a.month, a.int_mode, a.world, a.workload, a.steps, a.warmup,
-                      a.rl_price if rl else None, fh)
+                      a.rl_price if rl else None, fh, a.shard_of,
+                      (a.shard_rank if a.shard_rank == "max" else int(a.shard_rank)) if a.shard_of > 1 else None,
+                      a.steps_mode)
     ms, per, side_ms = trace_ms(os.path.join(a.prof, "trace", "trace_kernel_trace.csv"), a.steps, per_unit)
     out = {"workload": key, "command": a.command, "unit": "action" if rl else "step",
            "kernel_ms_per_step": ms, "kernel_ms_per_step_min_max": [min(per), max(per)],
