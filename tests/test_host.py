@@ -30,6 +30,18 @@ def test_library_exports_every_header_symbol(lib_path):
     assert lib.dragg_mpc_abi_version() == _lib.ABI_VERSION
 
 
+def test_results_library_exports_its_header():
+    """libdragg_results.so (the host-side results.json formatter) exports include/dragg_results.h."""
+    from dragg_amd import build as B
+    path = B.build_results()
+    names = re.findall(r"^\w[\w\s\*]*?\b(dragg_\w+)\s*\(", open(os.path.join(ROOT, "include", "dragg_results.h")).read(), re.M)
+    assert set(names) == {"dragg_results_abi_version", "dragg_fmt_double", "dragg_fmt_series"}
+    lib = ctypes.CDLL(path)
+    for n in names:
+        assert hasattr(lib, n), n
+    assert not B.results_needs_build()
+
+
 def test_ctypes_structs_match_c_layout(tmp_path):
     """sizeof/offsetof of every ABI struct, from gcc, against the ctypes mirrors."""
     from dragg_amd import _lib as L
