@@ -85,7 +85,11 @@ def parse(argv=None):
     ap.add_argument("--exact", action="store_true",
                     help="DRAGG_FLAG_EXACT (diagnostic): every chain the front DPs cannot take goes to the step-function DP")
     ap.add_argument("--no-overlap", action="store_true",
-                    help="rbo: serial steps (no lag mode: every home's step t completes before step t + 1 starts)")
+                    help="rbo: serial steps (no lag mode: every home's step t completes before step t + 1 starts); "
+                         "= --steps-mode serial")
+    ap.add_argument("--steps-mode", default="lag", choices=["lag", "adaptive", "serial"],
+                    help="rbo: lag (lag mode from the first step), adaptive (serial steps until a step hands a chain "
+                         "to the step-function DP, lag mode after), serial")
     ap.add_argument("--no-history", action="store_true",
                     help="skip the per-step history write (collected_data); a configs[2] run keeps it")
     ap.add_argument("--keep-crashing-homes", action="store_true",
@@ -527,7 +531,8 @@ def main():
                                int_mode=args.int_mode, seed=12, rank=shard_rank if shard else rank,
                                world=args.shard_of if shard else world,
                                keep_history=not args.no_history, exact=args.exact,
-                               overlap=not (rl or args.no_overlap))
+                               overlap=not (rl or args.no_overlap or args.steps_mode == "serial"),
+                               adaptive=args.steps_mode == "adaptive")
         if shard:
             agg.world = 1                     # one GPU: no collectives (the shard's own sums)
         stream = torch.cuda.current_stream()
@@ -655,6 +660,7 @@ def main():
             "history_written": not args.no_history,
             "lag_mode": bool(agg.overlap),
             "steps_mode": steps_mode(agg),
+            "lag_from_step": getattr(agg, "lag_from", None),
             "sim_wall_s": elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0,

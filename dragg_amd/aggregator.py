@@ -37,7 +37,8 @@ def shard_index(n, rank, world):
 class DeviceAggregator:
     def __init__(self, homes, oat, ghi, tou, start_index=0, num_timesteps=96, reward_price=(0.0,),
                  int_mode="round", seed=0, rank=0, world=1, group=None, keep_history=True,
-                 max_iter=4000, check_every=10, device=None, batch_cls=MPCBatch, exact=False, overlap=False):
+                 max_iter=4000, check_every=10, device=None, batch_cls=MPCBatch, exact=False, overlap=False,
+                 adaptive=False, ring=16):
         self.rank, self.world, self.group = rank, world, group
         self.seed = int(seed)
         # identifies the community a checkpoint belongs to (load_state refuses another one's)
@@ -67,25 +68,75 @@ class DeviceAggregator:
         # overlap (lag mode, MPCBatch.enable_lag): a home whose chain needs the slow step-function DP
         # finishes that step on a side stream while the others go on (run_rbo_mpc has no feedback
         # between homes, aggregator.py:757-778); its results land in the step's own history rows later,
-        # so the deferred sums are taken from those rows once the side stream has drained.  Needs the
-        # history and keyed season noise; int_mode round.
-        self.overlap = (bool(overlap) and self.hist is not None and int_mode in ("round", "fail") and n > 0
-                        and hasattr(self.batch, "enable_lag"))
+        # so the deferred sums are taken from those rows once the side stream has drained.  Without the
+        # history (keep_history=False, configs[3]: 100k homes x 672 steps) the steps write a ring of
+        # `ring` history rows instead, and the side stream sums row t right after step t's side pass (the
+        # main pass of step t + ring waits for that).  Keyed season noise; int_mode round.
+        self.overlap = (bool(overlap) and int_mode in ("round", "fail") and n > 0 and hasattr(self.batch, "enable_lag"))
+        self.ring = None
         if self.overlap:
-            self.batch.enable_lag()
+            if self.hist is None:
+                R = max(2, min(int(ring), num_timesteps))
+                self.ring = torch.full((R, L.NVAL, n), float("nan"), dtype=torch.float64, device=dev)
+                self.batch.enable_lag(ring=R)
+            else:
+                self.batch.enable_lag()
         self._unsummed = []          # lag-mode steps whose agg_hist row is not computed yet
+        # adaptive start (overlap): serial steps -- no side-stream launches at all -- until a step hands a
+        # chain to the step-function DP (int_path bit 15, read back asynchronously, the host kept at most
+        # FLAG_LAG steps ahead of the GPU), lag mode from the next step the host enqueues
+        self.adaptive = self.overlap and bool(adaptive)
+        self._lagging = self.overlap and not self.adaptive
+        if self.adaptive:
+            K = self.FLAG_LAG + 2
+            pin = torch.cuda.is_available() and dev.type == "cuda"
+            self._flag_host = torch.zeros(K, dtype=torch.int32, pin_memory=pin)
+            self._flag_ev = [torch.cuda.Event() if pin else None for _ in range(K)]
+            self._flag_step = [-1] * K
+            self.lag_from = None             # the first step run in lag mode
+
+    FLAG_LAG = 2                 # adaptive start: steps the host may run ahead of the last flag it reads
+
+    def _lag_now(self, t):
+        """Adaptive start: has a step the host can see (<= t - FLAG_LAG, waited for) listed a step-function
+        chain?  Then this and every later step runs in lag mode."""
+        if self._lagging:
+            return True
+        K = len(self._flag_step)
+        s = t - self.FLAG_LAG
+        if s >= 0 and self._flag_step[s % K] == s:
+            ev = self._flag_ev[s % K]
+            if ev is not None:
+                ev.synchronize()
+            if int(self._flag_host[s % K]):
+                self._lagging = True
+                self.lag_from = t
+        return self._lagging
+
+    def _flag(self, t):
+        """After a serial step t: did it hand a chain to the step-function DP?  (device -> pinned host, async)"""
+        K = len(self._flag_step)
+        f = ((self.batch.int_path & L.PATH_STEPS) != 0).any().to(torch.int32)
+        self._flag_host[t % K:t % K + 1].copy_(f.reshape(1), non_blocking=True)
+        if self._flag_ev[t % K] is not None:
+            self._flag_ev[t % K].record()
+        self._flag_step[t % K] = t
 
     # aggregator.py:711-726
     def run_iteration(self, noise=None):
         t = self.timestep
         hist = self.hist[t] if self.hist is not None else None
-        if self.overlap and noise is None:
-            self.batch.step_lagged(t, hist, self.status_hist[t], path_row=self.path_hist[t])
+        if self.overlap and noise is None and self._lag_now(t):
+            ring = self.ring is not None
+            self.batch.step_lagged(t, self.ring[t % self.ring.shape[0]] if ring else hist, self.status_hist[t],
+                                   path_row=self.path_hist[t], sums_row=self.agg_hist[t] if ring else None)
         else:
             self.batch.step(t, noise=noise, hist=hist)
             self.status_hist[t].copy_(self.batch.status, non_blocking=True)
             if hasattr(self.batch, "int_path"):
                 self.path_hist[t].copy_(self.batch.int_path, non_blocking=True)
+            if self.adaptive and noise is None:
+                self._flag(t)
         self.timestep += 1
 
     def approx_counts(self, lo=0, hi=None):
@@ -130,8 +181,10 @@ class DeviceAggregator:
         one collective; the ranks then need not meet at every step."""
         t = self.timestep - 1
         if self.overlap and defer and self.batch.lag["next"] == self.timestep:
-            # (lag mode: the lagging homes' fields of step t are not written yet; drain() sums the row)
-            self._unsummed.append(t)
+            # (lag mode: the lagging homes' fields of step t are not written yet; drain() sums the row --
+            # with the history ring, the side stream already does, after the step's side pass)
+            if self.ring is None:
+                self._unsummed.append(t)
             if self.world > 1:
                 self._deferred.append(t)
             return None

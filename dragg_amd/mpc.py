@@ -266,16 +266,17 @@ class MPCBatch:
                 "pending": False,               # side work not yet joined into the main stream
             }
 
-    def step_lagged(self, t, hist, status_row, stream=None, path_row=None):
+    def step_lagged(self, t, hist, status_row, stream=None, path_row=None, sums_row=None):
         """One timestep in lag mode: the main pass on `stream` (default: the current one), the side pass
         on the side stream after it.  `hist` ([NVAL][N]), `status_row` ([N] int32) and `path_row` ([N]
         int32, the int_path bits; default self.int_path) receive the step's per-home results -- a
         lagging home's later -- so they must be this step's own rows; nothing of the step may be read
-        before drain()."""
+        before drain().  `sums_row` ([3] f64, optional): collect_data's sums of the step, from `hist`,
+        computed on the side stream after the step's side pass (dragg_mpc_aggregate_rows)."""
         with torch.cuda.device(self.device):
-            return self._step_lagged(t, hist, status_row, stream, path_row)
+            return self._step_lagged(t, hist, status_row, stream, path_row, sums_row)
 
-    def _step_lagged(self, t, hist, status_row, stream, path_row=None):
+    def _step_lagged(self, t, hist, status_row, stream, path_row=None, sums_row=None):
         lg = self.lag
         if lg is None:
             raise RuntimeError("enable_lag() first")
@@ -302,12 +303,15 @@ class MPCBatch:
         side.wait_event(lg["main_done"])
         L.check(self.lib.dragg_mpc_step_side(ctypes.byref(self.dims), ctypes.byref(prob), ctypes.byref(hsh),
                                              ctypes.byref(out), int(t), ctypes.byref(lag), L.stream_ptr(side, self.device)))
+        if sums_row is not None:
+            L.check(self.lib.dragg_mpc_aggregate_rows(ctypes.byref(self.dims), L.ptr(hist), 1, L.ptr(sums_row),
+                                                      L.stream_ptr(side, self.device)))
         lg["side_done"][slot].record(side)
         lg["recorded"][slot] = True
         lg["last"] = slot
         lg["next"] = t + 1
         lg["pending"] = True
-        self._keep = (hist, status_row, path_row)
+        self._keep = (hist, status_row, path_row, sums_row)
 
     def drain(self, stream=None):
         """Join the side stream into `stream` (default: the current one): after this, everything the

@@ -27,13 +27,14 @@ def _bench_community():
     return homes, oat, ghi, tou
 
 
-def _run(overlap, rank, world, com):
+def _run(overlap, rank, world, com, adaptive=False, keep_history=True, steps=STEPS):
     homes, oat, ghi, tou = com
-    agg = DeviceAggregator(homes, oat, ghi, tou, 0, STEPS, reward_price=[0.0], seed=12, rank=rank, world=world,
-                           overlap=overlap)
+    agg = DeviceAggregator(homes, oat, ghi, tou, 0, steps, reward_price=[0.0], seed=12, rank=rank, world=world,
+                           overlap=overlap, adaptive=adaptive, keep_history=keep_history)
     agg.world = 1                              # one GPU: the shard's own sums, no collectives
-    assert agg.overlap == overlap
-    for _ in range(STEPS):
+    assert agg.overlap == overlap and agg.adaptive == (overlap and adaptive)
+    assert (agg.ring is not None) == (overlap and not keep_history)
+    for _ in range(steps):
         agg.run_iteration()
         agg.collect_data(defer=True)
     agg.reduce_history()
@@ -68,3 +69,47 @@ def test_overlap_is_bit_identical_to_serial(com, rank, world, gpu):
     assert np.array_equal(_bits(a.batch.fc_store), _bits(b.batch.fc_store))
     # the lagged sums are collect_data's on the final state too
     assert np.array_equal(_bits(b.agg_hist[STEPS - 1]), _bits(b.batch.aggregate()))
+
+
+@pytest.mark.parametrize("adaptive,keep_history", [(True, True), (False, False), (True, False)])
+def test_adaptive_start_and_history_ring_bit_identical(com, adaptive, keep_history, gpu):
+    """The adaptive start (serial steps until one lists a step-function chain, then lag mode) and lag mode
+    without the history (a ring of 16 history rows, the sums taken on the side stream after each step's side
+    pass) give the serial run's results bit for bit, on the 8-way shard holding home 7519."""
+    rank, world = 7519 % 8, 8
+    a = _run(False, rank, world, com)
+    b = _run(True, rank, world, com, adaptive=adaptive, keep_history=keep_history)
+    if adaptive:
+        assert b.lag_from is not None and 36 < b.lag_from <= 36 + b.FLAG_LAG + 1, b.lag_from
+    assert np.array_equal(a.status_hist.cpu().numpy(), b.status_hist.cpu().numpy())
+    assert np.array_equal(a.path_hist.cpu().numpy(), b.path_hist.cpu().numpy())
+    assert np.array_equal(_bits(a.agg_hist), _bits(b.agg_hist))
+    assert np.array_equal(_bits(a.batch.vals), _bits(b.batch.vals))
+    assert np.array_equal(_bits(a.batch.fc_store), _bits(b.batch.fc_store))
+    if keep_history:
+        assert np.array_equal(_bits(a.hist), _bits(b.hist))
+    c = b.approx_counts()
+    assert c["approx_solves"] == 0 and c["step_dp_solves"] > 0
+
+
+def test_seven_days_ring_lag_bit_identical(gpu):
+    """configs[3]'s shape (a 7-day run at 15-min steps without the per-step history, keep_history=False) in
+    lag mode on the ring, at reduced N: the 8-way shard of the bench community holding home 7519 (its
+    step-function chains recur every day), 672 steps: bit-identical to serial steps."""
+    dt, hh, steps = 4, 12, 672
+    days = math.ceil((math.ceil(steps / dt) + hh + 2) / 24) + 1
+    homes = synthetic_homes(10000, seed=12, days=days, dt=dt, horizon_hours=hh)
+    oat, ghi, tou = synthetic_weather(days, dt, math.ceil(steps / dt), seed=3, month=7)
+    com7 = (homes, oat, ghi, tou)
+    rank, world = 7519 % 8, 8
+    a = _run(False, rank, world, com7, keep_history=False, steps=steps)
+    b = _run(True, rank, world, com7, keep_history=False, steps=steps)
+    assert b.ring is not None and b.ring.shape[0] == 16
+    assert np.array_equal(a.status_hist.cpu().numpy(), b.status_hist.cpu().numpy())
+    assert np.array_equal(a.path_hist.cpu().numpy(), b.path_hist.cpu().numpy())
+    assert np.array_equal(_bits(a.agg_hist), _bits(b.agg_hist))
+    assert np.array_equal(_bits(a.batch.vals), _bits(b.batch.vals))
+    assert np.array_equal(_bits(a.batch.fc_store), _bits(b.batch.fc_store))
+    steps_dp = ((a.path_hist.cpu().numpy() & (1 << 15)) != 0).sum(axis=1)
+    print(f"7 days: step-function solves per day {[int(steps_dp[d * 96:(d + 1) * 96].sum()) for d in range(7)]}")
+    assert steps_dp.sum() > 0

@@ -19,6 +19,10 @@ args_of() {
   case $1 in
     driver) echo --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 ;;
     drivers) echo --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --no-overlap ;;
+    drivera) echo --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --steps-mode adaptive ;;
+    full96a) echo --steps 96 --warmup 4 --cpu-seconds 0 --steps-mode adaptive ;;
+    shard8r7a) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 --shard-rank 7 --steps-mode adaptive ;;
+    cfg3a) echo --homes 100000 --horizon-hours 6 --steps 24 --warmup 2 --cpu-seconds 0 --no-history ;;
     shard8r7) echo --steps 96 --warmup 4 --cpu-seconds 0 --shard-of 8 --shard-rank 7 ;;
     shard8r7d) echo --steps 20 --warmup 5 --cpu-seconds 0 --shard-of 8 --shard-rank 7 ;;
     shard8r0d) echo --steps 20 --warmup 5 --cpu-seconds 0 --shard-of 8 --shard-rank 0 ;;
