@@ -76,6 +76,11 @@ constexpr int RS_HOLD = 4;               // ILP = 2 front DP: child pairs held i
 // exact pass's fronts then hold 22-280 labels, where the LP bound and the bucketed schedule's cost left
 // 30 % of the chains past 2,048)
 constexpr int NCELL = 1024;              // cells of the grid
+// a row of the cell bound in the workspace: NCELL 16-bit codes and its (offset, scale) as two f32; code q is the
+// lower bound offset + q scale (rounded DOWN at encoding, so it stays below the f32 row it stands for),
+// 0xFFFF is +inf.  Half the bytes of f32 rows (2 GB per launch at 10k homes, H = 48, round 5)
+constexpr int CELL_STRIDE = NCELL + 4;
+constexpr unsigned CELL_INF = 0xFFFFu;
 constexpr int BEAM_K = 32;               // labels a beam stage keeps (7 BEAM_K children fit NF_MID; measured
                                          //   RL action at 48: 20.1 ms, 32: 19.6 ms)
 constexpr int CELL_TRIES = 8;            // bisection steps on the bound after a pass past the capacity
@@ -1538,12 +1543,12 @@ __host__ __device__ inline size_t w_region_bytes(int N, int H) { return (size_t)
 // the lag mode's side workspace: the lists and per-block scratch [defer_offset, w_region_offset)
 __host__ __device__ inline size_t side_workspace_bytes(int N, int H) { return w_region_offset(N, H) - defer_offset(N, H); }
 // then (256-aligned), with a reward-price list (dims.n_rp > 1: RL prices possible), the cell bound's
-// rows of every home's indoor-air chain [N][H + 1][NCELL] f32 (cell_kernel; row 0, cell 0: 1 = valid)
+// rows of every home's indoor-air chain [N][H + 1][CELL_STRIDE] u16 codes (cell_kernel; row 0: the valid flag)
 __host__ __device__ inline size_t cell_region_offset(int N, int H) {
     return (w_region_offset(N, H) + w_region_bytes(N, H) + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t cell_region_bytes(int N, int H, bool cells) {
-    return cells ? (size_t)N * (H + 1) * NCELL * sizeof(float) : 0;
+    return cells ? (size_t)N * (H + 1) * CELL_STRIDE * sizeof(uint16_t) : 0;
 }
 __host__ __device__ inline size_t direct_workspace_bytes(int N, int H, bool cells) {
     return cell_region_offset(N, H) + cell_region_bytes(N, H, cells);
@@ -2382,7 +2387,7 @@ struct FrontBufs {
     double *wlx, *wlv, *wls;             // [WAVE] LDS: the current stage's W (points, slopes)
     char* xch;                           // [xch_bytes(CAP)] LDS: the waves' exchange area (NW > 1)
     // dp_front<..., CELL = true>: the cell bound in place of W
-    const float* cg;                     // [H + 1][NCELL] global: cell_rows' lower bounds of x_k's cost-to-go
+    const uint16_t* cg;                  // [H + 1][CELL_STRIDE] global: cell_rows' lower bounds of x_k's cost-to-go
     double c_lo, c_inv;                  // the grid: cell of x = floor((x - c_lo) c_inv)
 };
 
@@ -2457,6 +2462,45 @@ DEV T dpp_iscan(T v, int lane, T id, Op op) {
 // x_{k+1}'s box (+inf where none) -- a minimum over a superset of the states a schedule can reach,
 // rounded down to f32.  r0 / r1: two LDS rows of scratch (NCELL + 1 floats each at least).  Every thread of the block calls it; false
 // (no bound) on a degenerate stage (A <= 0).
+// a cell's lower bound from a quantized row (offset + q scale, +inf for CELL_INF)
+DEV float cell_dec(const uint16_t* row, int c) {
+    const unsigned q = row[c];
+    const float* const hd = reinterpret_cast<const float*>(row + NCELL);
+    return q == CELL_INF ? INFINITY : fmaf((float)q, hd[1], hd[0]);
+}
+// row 0 of a home's cell rows holds no bound: its header's first float flags the rows valid (1)
+DEV bool cell_rows_valid(const uint16_t* cg) { return reinterpret_cast<const float*>(cg + NCELL)[0] == 1.0f; }
+// a row of NT threads' f32 values (LDS) to its 16-bit codes: offset = the least finite value, scale = the
+// finite range / 65534 rounded up; each code rounded down until its decoded value is at most the value
+template <int NT>
+DEV void cell_store(uint16_t* row, const float* v, int tid) {
+    __shared__ float red[2][NT / WAVE];
+    float lo = INFINITY, hi = -INFINITY;
+    for (int j = tid; j < NCELL; j += NT)
+        if (v[j] < INFINITY) { lo = fminf(lo, v[j]); hi = fmaxf(hi, v[j]); }
+    lo = dpp_reduce(lo, [](float a, float b) { return fminf(a, b); });
+    hi = dpp_reduce(hi, [](float a, float b) { return fmaxf(a, b); });
+    if ((tid & (WAVE - 1)) == 0) { red[0][tid / WAVE] = lo; red[1][tid / WAVE] = hi; }
+    __syncthreads();
+    lo = INFINITY; hi = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NT / WAVE; ++w) { lo = fminf(lo, red[0][w]); hi = fmaxf(hi, red[1][w]); }
+    const bool any = lo < INFINITY;
+    const float off = any ? lo : 0.0f;
+    const float sc = any && hi > lo ? __double2float_ru(((double)hi - (double)lo) / 65534.0) : 0.0f;
+    for (int j = tid; j < NCELL; j += NT) {
+        const float x = v[j];
+        unsigned q = CELL_INF;
+        if (x < INFINITY) {
+            q = sc > 0.0f ? (unsigned)fmin(65534.0, fmax(0.0, floor(((double)x - (double)off) / (double)sc))) : 0u;
+            while (q > 0 && fmaf((float)q, sc, off) > x) --q;
+        }
+        row[j] = (uint16_t)q;
+    }
+    if (tid == 0) { reinterpret_cast<float*>(row + NCELL)[0] = off; reinterpret_cast<float*>(row + NCELL)[1] = sc; }
+    __syncthreads();                                     // (red is reused by the next row)
+}
+
 // the cell grid over a chain's box [bl, bh] (widened past every tolerance of the labels' box tests)
 DEV void cell_grid(double bl, double bh, double& c_lo, double& c_inv) {
     auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
@@ -2465,7 +2509,7 @@ DEV void cell_grid(double bl, double bh, double& c_lo, double& c_inv) {
 }
 
 template <int NT, int SS>
-DEV bool cell_rows(float* cg, float* r0, float* r1, const double* cA, const double* cC, const double* cq, int H, int S,
+DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const double* cC, const double* cq, int H, int S,
                    double g, double lo0, double hi0, double lo, double hi, double c_lo, double c_inv, int tid) {
     auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
     const double dlt = 1.0 / c_inv;
@@ -2482,13 +2526,10 @@ DEV bool cell_rows(float* cg, float* r0, float* r1, const double* cA, const doub
     {
         int c0, c1;
         cell_span(bxl(H), bxh(H), c0, c1);
-        for (int j = tid; j < NCELL; j += NT) {
-            const float v = (j >= c0 && j <= c1) ? 0.0f : INFINITY;
-            r0[j] = v;
-            cg[(size_t)H * NCELL + j] = v;
-        }
+        for (int j = tid; j < NCELL; j += NT) r0[j] = (j >= c0 && j <= c1) ? 0.0f : INFINITY;
     }
     __syncthreads();
+    cell_store<NT>(cg + (size_t)H * CELL_STRIDE, r0, tid);
     float* nxt = r0;
     float* cur = r1;
     for (int k = H - 1; k >= 1; --k) {
@@ -2540,9 +2581,10 @@ DEV bool cell_rows(float* cg, float* r0, float* r1, const double* cA, const doub
 #pragma unroll
             for (int r = 0; r < (NCELL + NT - 1) / NT; ++r) {
                 const int j = r * NT + tid;
-                if (j < NCELL) { cur[j] = outv[r]; cg[(size_t)k * NCELL + j] = outv[r]; }
+                if (j < NCELL) cur[j] = outv[r];
             }
             __syncthreads();
+            cell_store<NT>(cg + (size_t)k * CELL_STRIDE, cur, tid);
             float* t_ = nxt; nxt = cur; cur = t_;
             continue;
         }
@@ -2574,11 +2616,10 @@ DEV bool cell_rows(float* cg, float* r0, float* r1, const double* cA, const doub
                     if (m < INFINITY) best = fmin(best, fma(q, (double)u, (double)m));
                 }
             }
-            const float v = best < INFINITY ? __double2float_rd(best) : INFINITY;
-            cur[j] = v;
-            cg[(size_t)k * NCELL + j] = v;
+            cur[j] = best < INFINITY ? __double2float_rd(best) : INFINITY;
         }
         __syncthreads();
+        cell_store<NT>(cg + (size_t)k * CELL_STRIDE, cur, tid);
         float* t_ = nxt; nxt = cur; cur = t_;
     }
     return true;
@@ -2817,10 +2858,10 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     bool tried = CELL || prune || B.wg == nullptr;   // the bound is built at most once
     // the cell bound's row of the stage's children, read from the workspace (cell_kernel's rows: staging
     // them in LDS cost a block per CU of the mid launch, measured slower)
-    const float* crow = B.cg + NCELL;
+    const uint16_t* crow = B.cg + CELL_STRIDE;
     auto cell_at = [&](double x) -> double {
         const int c = min(NCELL - 1, max(0, (int)floor((x - B.c_lo) * B.c_inv)));
-        return (double)crow[c];
+        return (double)cell_dec(crow, c);
     };
     auto bound_at = [&](double x, int wst_) -> double {
         if constexpr (CELL) return cell_at(x); else return w_eval(B, x, wst_);
@@ -3312,7 +3353,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         }
         for (int b = tid; b < NBK && !nodom; b += NT) { B.kb[2 * b] = ~0ull; B.cb[2 * b] = 0ull; }
         if constexpr (CELL) {
-            crow = B.cg + (size_t)(k + 2) * NCELL;
+            crow = B.cg + (size_t)(k + 2) * CELL_STRIDE;
         } else if (prune && k + 1 < H && wid == 0) {
             w_to_lds(B, lane, wnext.x, wnext.y);
             if (k + 3 <= H) wnext = load_row(k + 3);
@@ -4566,9 +4607,9 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                     : reinterpret_cast<uint16_t*>(lw + big_region_offset(N, H)) + (size_t)slot * H * NF_BIG;
                 // RL prices: the cell bound of the indoor-air chain (cell_kernel's rows of this home, before the
                 // mid launch); the tank chain keeps the LP bound (its fronts stay small under RL prices)
-                float* const cg = reinterpret_cast<float*>(ws + cell_region_offset(N, H)) + (size_t)home * (H + 1) * NCELL;
+                uint16_t* const cg = reinterpret_cast<uint16_t*>(ws + cell_region_offset(N, H)) + (size_t)home * (H + 1) * CELL_STRIDE;
                 double c_lo = 0.0, c_inv = 0.0;
-                const bool have_cells = SECOND && rl_prices && h.S == 6 && chain == 0 && a.d.n_rp > 1 && cg[0] == 1.0f;
+                const bool have_cells = SECOND && rl_prices && h.S == 6 && chain == 0 && a.d.n_rp > 1 && cell_rows_valid(cg);
                 if (have_cells) cell_grid(fmin(lo0, lo), fmax(hi0, hi), c_lo, c_inv);
                 const FrontBufs FB{reinterpret_cast<double2*>(sb + bl.fa), reinterpret_cast<double2*>(sb + bl.fb),
                                    reinterpret_cast<unsigned long long*>(sb + bl.kb),
@@ -4640,7 +4681,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                                     const double tl = lo0 - TOL_P * (1 + fabs(lo0)), th = hi0 + TOL_P * (1 + fabs(hi0));
                                     if (x1 >= tl && x1 <= th)
                                         v = fma(D.cq[0], (double)u,
-                                                (double)cg[NCELL + min(NCELL - 1, max(0, (int)floor((x1 - c_lo) * c_inv)))]);
+                                                (double)cell_dec(cg + CELL_STRIDE, min(NCELL - 1, max(0, (int)floor((x1 - c_lo) * c_inv)))));
                                 }
                                 lo_u = dpp_reduce(v, [](double a_, double b_) { return fmin(a_, b_); });
                             }
@@ -4814,13 +4855,13 @@ __global__ __launch_bounds__(NT_CELL, 4) void cell_kernel(KArgs a) {
         __syncthreads();
         double c_lo, c_inv;
         cell_grid(h.Tmin, h.Tmax, c_lo, c_inv);
-        float* const cg = reinterpret_cast<float*>(ws + cell_region_offset(N, H)) + (size_t)home * (H + 1) * NCELL;
+        uint16_t* const cg = reinterpret_cast<uint16_t*>(ws + cell_region_offset(N, H)) + (size_t)home * (H + 1) * CELL_STRIDE;
         pf.mark(DRAGG_PH_CHECK);                   // (diagnostic: the prologue, in the check slot)
         const bool ok = cell_rows<NT_CELL, 6>(cg, r0, r1, D.cA, D.cC, D.cq, H, 6, h.g, h.Tmin, h.Tmax, h.Tmin, h.Tmax,
                                               c_lo, c_inv, tid);
         pf.mark(DRAGG_PH_FACTOR);                  // (diagnostic: the cell rows, in the factor slot)
         if (tid == 0) {
-            cg[0] = ok ? 1.0f : 0.0f;
+            reinterpret_cast<float*>(cg + NCELL)[0] = ok ? 1.0f : 0.0f;
             if (pf.on) {
                 a.out.cycles[(size_t)DRAGG_PH_CHECK * N + home] = (int64_t)pf.acc[DRAGG_PH_CHECK];
                 a.out.cycles[(size_t)DRAGG_PH_FACTOR * N + home] = (int64_t)pf.acc[DRAGG_PH_FACTOR];

@@ -92,15 +92,19 @@ def test_adaptive_start_and_history_ring_bit_identical(com, adaptive, keep_histo
     assert c["approx_solves"] == 0 and c["step_dp_solves"] > 0
 
 
-def test_seven_days_ring_lag_bit_identical(gpu):
+def test_seven_days_ring_lag_bit_identical(com, gpu):
     """configs[3]'s shape (a 7-day run at 15-min steps without the per-step history, keep_history=False) in
-    lag mode on the ring, at reduced N: the 8-way shard of the bench community holding home 7519 (its
-    step-function chains recur every day), 672 steps: bit-identical to serial steps."""
-    dt, hh, steps = 4, 12, 672
-    days = math.ceil((math.ceil(steps / dt) + hh + 2) / 24) + 1
-    homes = synthetic_homes(10000, seed=12, days=days, dt=dt, horizon_hours=hh)
-    oat, ghi, tou = synthetic_weather(days, dt, math.ceil(steps / dt), seed=3, month=7)
-    com7 = (homes, oat, ghi, tou)
+    lag mode on the ring, at reduced N: the 8-way shard of the bench community holding home 7519, its weather
+    and water draws repeated day after day (so its step-function chains of day 1 recur), 672 steps:
+    bit-identical to serial steps."""
+    import copy
+    steps, reps = 672, 9
+    homes, oat, ghi, tou = com
+    homes = copy.deepcopy(homes)
+    for h in homes:
+        h["wh"]["draw_sizes"] = list(h["wh"]["draw_sizes"][:24]) * (reps * len(h["wh"]["draw_sizes"]) // 24)
+    day = 24 * 4
+    com7 = (homes, list(oat[:day]) * reps * 2, list(ghi[:day]) * reps * 2, list(tou[:day]) * reps * 2)
     rank, world = 7519 % 8, 8
     a = _run(False, rank, world, com7, keep_history=False, steps=steps)
     b = _run(True, rank, world, com7, keep_history=False, steps=steps)
