@@ -111,14 +111,44 @@ def write_results(rdir, case, collected):
     return path
 
 
-def write_results_history(rdir, case, all_homes, checked, hist, summary_):
+def _summary_part(summary_, lead):
+    pieces, lists = [], []
+    _layout(summary_, 1, pieces, lists)
+    num = format_float_lists(lists)
+    out = [(lead + '"Summary": ').encode("ascii")]
+    for p in pieces:
+        out.append(p.encode("ascii") if type(p) is str else num[p])
+    out.append(b"\n}")
+    return b"".join(out)
+
+
+def write_results_history(rdir, case, all_homes, checked, hist, summary_, cache=None):
     """write_results(rdir, case, collected) for collected = new_collected(all_homes) + append_history(
     checked, hist) + {"Summary": summary_}, the same bytes, without building the Python lists: every
     home's series comes out of the history array [T][NVAL][len(checked)] (NaN = absent, skipped) and
     goes to the formatter in one call.  Falls back to the generic writer when a home's initial entry
-    is not a float (json.dump would render an int as an int)."""
+    is not a float (json.dump would render an int as an int).
+
+    `cache` (a dict the caller keeps): a rewrite of the same file for the same history (the reference
+    writes results.json at the last checkpoint and again at the end, aggregator.py:768-778, 941-970,
+    with only the Summary's solve_time new) keeps the file's homes part and rewrites the Summary."""
     hist = np.asarray(hist, dtype=np.float64)
     T = hist.shape[0]
+    path = os.path.join(rdir, case, "results.json")
+    sig = (id(all_homes), len(all_homes), id(checked), len(checked), hist.shape,
+           hash(hist[-1].tobytes()) if T else 0)
+    if cache is not None and path in cache and os.path.isfile(path):
+        c_sig, prefix, size, mtime = cache[path]
+        st = os.stat(path)
+        if c_sig == sig and st.st_size == size and st.st_mtime_ns == mtime:
+            tail = _summary_part(summary_, ",\n    " if all_homes else "{\n    ")
+            with open(path, "r+b") as f:
+                f.seek(prefix)
+                f.write(tail)
+                f.truncate()
+            st = os.stat(path)
+            cache[path] = (sig, prefix, st.st_size, st.st_mtime_ns)
+            return path
     init_keys = ("temp_in_opt", "temp_wh_opt", "e_batt_opt")
 
     def init_of(h, k):
@@ -187,7 +217,6 @@ def write_results_history(rdir, case, all_homes, checked, hist, summary_):
     sp8 = "\n" + " " * 8
     case_dir = os.path.join(rdir, case)
     os.makedirs(case_dir, exist_ok=True)
-    path = os.path.join(case_dir, "results.json")
     out, size = [], 0
     with open(path, "wb") as f:
         lead = "{\n    "
@@ -222,14 +251,12 @@ def write_results_history(rdir, case, all_homes, checked, hist, summary_):
             if size > (1 << 20):
                 f.write(b"".join(out))
                 out, size = [], 0
-        pieces, lists = [], []
-        _layout(summary_, 1, pieces, lists)
-        num = format_float_lists(lists)
-        out.append((lead + '"Summary": ').encode("ascii"))
-        for p in pieces:
-            out.append(p.encode("ascii") if type(p) is str else num[p])
-        out.append(b"\n}")
         f.write(b"".join(out))
+        prefix = f.tell()
+        f.write(_summary_part(summary_, lead))
+    if cache is not None:
+        st = os.stat(path)
+        cache[path] = (sig, prefix, st.st_size, st.st_mtime_ns)
     return path
 
 

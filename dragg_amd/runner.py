@@ -379,7 +379,10 @@ class Aggregator:
             self._collected = None
         with self._phase("results_write"):
             # the same bytes as json.dump(collected_data, indent=4), straight from the history array
-            return R.write_results_history(self.run_dir, self.case, self.all_homes, self.checked, hist, summary)
+            if not hasattr(self, "_results_cache"):
+                self._results_cache = {}
+            return R.write_results_history(self.run_dir, self.case, self.all_homes, self.checked, hist, summary,
+                                           cache=self._results_cache)
 
     @property
     def collected_data(self):

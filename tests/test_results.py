@@ -148,6 +148,14 @@ def test_history_writer_is_json_dump_of_collected_data(tmp_path, T):
     c["Summary"] = summary
     with open(path) as f:
         assert f.read() == json.dumps(c, indent=4)
+    # a rewrite for the same history (the final write after the last checkpoint): Summary only, same bytes
+    cache = {}
+    R.write_results_history(str(tmp_path), "c", homes, checked, hist, summary, cache=cache)
+    summary2 = dict(summary, solve_time=2.5)
+    path = R.write_results_history(str(tmp_path), "c", homes, checked, hist, summary2, cache=cache)
+    c["Summary"] = summary2
+    with open(path) as f:
+        assert f.read() == json.dumps(c, indent=4)
     # an int initial entry: json.dump writes it as an int -- the writer falls back to the generic path
     homes[0]["hvac"]["temp_in_init"] = 20
     path = R.write_results_history(str(tmp_path), "b2", homes, checked, hist, summary)
