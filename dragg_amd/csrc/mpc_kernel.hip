@@ -1244,6 +1244,7 @@ struct KArgs {
     int side;              // 1 in the side pass: its completions publish with a release
     int step_pool_cap;     // the step-function DP's pool per chain (POOL_CAP; a diagnostic knob shrinks it)
     long long step_work_cap;   // ... its work bound per pass (0: STEP_WORK_CAP)
+    int narrow_lds;        // the step-function launch's LDS bytes per block (0: all a CU has, narrow_layout)
 };
 
 // a clock value the side pass wrote: the reader must acquire before it reads the home's rows
@@ -1650,7 +1651,7 @@ __host__ __device__ inline int direct_lds_bytes(int H, int S) { return direct_la
 // recovery's duty values, L_k's table, then a pool with the rest of the CU's LDS: per stage V_{k+1}
 // (B, V) and the merge buffers (keys f64 x 2, ids i32 x 2) where they fit
 struct NarrowLayout { int off, cnt, wc, lc, red, xr, rng, rl, rh, dlo, dhi, xv, lt, sp, spb, bytes; };
-__host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
+__host__ __device__ inline NarrowLayout narrow_layout(int H, int S, int lds_cap = 0) {
     NarrowLayout o{};
     int p = direct_layout(H, S).bytes;
     auto take = [&](int bytes, int align) { p = (p + align - 1) / align * align; const int r = p; p += bytes; return r; };
@@ -1669,7 +1670,10 @@ __host__ __device__ inline NarrowLayout narrow_layout(int H, int S) {
     o.lt = take(8 * (3 * WAVE + 2), 16);
     // the pool takes what is left of the CU's LDS (>= the waves' PL tables of lp_cut)
     o.sp = take(0, 16);
-    o.spb = max(NT_STEPS / 64 * 6 * WAVE * 8, ((160 * 1024 - 256) - o.sp - 64) / 64 * 64);
+    // (lds_cap > 0, DRAGG_NARROW_LDS_KB: a smaller block that shares a CU with hot-launch blocks -- it need
+    // not wait for a CU to drain completely -- at the price of stages that spill to the workspace sooner)
+    const int cap_ = lds_cap > 0 ? min(lds_cap, 160 * 1024 - 256) : 160 * 1024 - 256;
+    o.spb = max(NT_STEPS / 64 * 6 * WAVE * 8, (cap_ - o.sp - 64) / 64 * 64);
     p = o.sp + o.spb;
     o.bytes = (p + 15) / 16 * 16;
     return o;
@@ -4424,7 +4428,7 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
             double2* const wg = reinterpret_cast<double2*>(ws + w_region_offset(N, H)) + (size_t)home * (H + 1) * WAVE;
             if constexpr (MODE == DM_NARROW) {
                 // the exact step-function DP (any prices, any feasible sets)
-                const NarrowLayout nl = narrow_layout(H, a.d.sub_steps);
+                const NarrowLayout nl = narrow_layout(H, a.d.sub_steps, a.narrow_lds);
                 char* const sb = reinterpret_cast<char*>(smem);
                 double* const sw = reinterpret_cast<double*>(lw + narrow_region_offset(N, H) +
                                                              (size_t)slot * step_slot_bytes());
@@ -5010,6 +5014,7 @@ struct Knobs {
     long long step_work_cap = 0;      //   capacity path); DRAGG_STEP_WORK_CAP: its work bound (0: default)
     int side_grid[4] = {0, 0, 0, 0};  // DRAGG_SIDE_GRID=hot,mid,big,narrow: the side pass's blocks (A/B)
     int ilp = 0;                      // DRAGG_HOT_ILP=1|2: the hot launch's chunks per pass (0: by N, hot_ilp)
+    int narrow_lds = 0;               // DRAGG_NARROW_LDS_KB=n: the step-function launch's LDS per block (A/B)
 };
 Knobs read_knobs() {
     Knobs r;
@@ -5023,6 +5028,8 @@ Knobs read_knobs() {
     if (wc && atoll(wc) > 0) r.step_work_cap = atoll(wc);
     const char* sg = getenv("DRAGG_SIDE_GRID");
     if (sg) sscanf(sg, "%d,%d,%d,%d", &r.side_grid[0], &r.side_grid[1], &r.side_grid[2], &r.side_grid[3]);
+    const char* nk = getenv("DRAGG_NARROW_LDS_KB");
+    if (nk && atoi(nk) > 0) r.narrow_lds = min(atoi(nk), 159) * 1024;
     const char* il = getenv("DRAGG_HOT_ILP");
     if (il && (il[0] == '1' || il[0] == '2') && il[1] == 0) r.ilp = il[0] - '0';
     return r;
@@ -5090,6 +5097,7 @@ int launch(const KArgs& a, hipStream_t s) {
     b.force_steps = knobs().force_steps;
     b.step_pool_cap = knobs().step_pool_cap;
     b.step_work_cap = knobs().step_work_cap;
+    b.narrow_lds = knobs().narrow_lds;
     // each list's length and the persistent launch's take counter after it, in one tiny launch
     // (three 8-byte memsets cost three fills: ~13 us of a 0.49 ms step at 1,250 homes)
     hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, nlen, blen, nullptr, nullptr);
@@ -5118,7 +5126,7 @@ int launch(const KArgs& a, hipStream_t s) {
                                   NW_BIG * WAVE, (size_t)big_layout(a.d.horizon, a.d.sub_steps).bytes, s);
     if (rc2) return rc2;
     const int rcn = launch_kernel(mpc_direct_kernel<EXPLICIT, DM_NARROW, NT_STEPS / WAVE>, attr[5], b, min(N, NARROW_SLOTS),
-                                  NT_STEPS, (size_t)narrow_layout(a.d.horizon, a.d.sub_steps).bytes, s);
+                                  NT_STEPS, (size_t)narrow_layout(a.d.horizon, a.d.sub_steps, b.narrow_lds).bytes, s);
     return rcn;
 }
 
@@ -5166,6 +5174,7 @@ int launch_lag(const KArgs& a, bool side, hipStream_t s) {
     b.force_steps = knobs().force_steps;
     b.step_pool_cap = knobs().step_pool_cap;
     b.step_work_cap = knobs().step_work_cap;
+    b.narrow_lds = knobs().narrow_lds;
     const size_t lds = kernel_lds_bytes(&a.d);
     if (!side) {
         hipLaunchKernelGGL(reset_lists_kernel, dim3(1), dim3(WAVE), 0, s, len, blen, a.skip + N, a.nar + N, nullptr);
@@ -5203,7 +5212,7 @@ int launch_lag(const KArgs& a, bool side, hipStream_t s) {
     if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_BUCKET, NW_BIG>, attr[2], b, grid[2],
                                 NW_BIG * WAVE, (size_t)big_layout(H, a.d.sub_steps).bytes, s);
     if (!rc) rc = launch_kernel(mpc_direct_kernel<false, DM_NARROW, NT_STEPS / WAVE>, attr[5], b,
-                                grid[3], NT_STEPS, (size_t)narrow_layout(H, a.d.sub_steps).bytes, s);
+                                grid[3], NT_STEPS, (size_t)narrow_layout(H, a.d.sub_steps, b.narrow_lds).bytes, s);
     return rc;
 }
 
@@ -5380,7 +5389,7 @@ int dragg_mpc_kernel_info_get(const dragg_mpc_dims* dims, dragg_mpc_kernel_info*
     if (!r) r = one((const void*)mpc_direct_kernel<false, DM_MID, NW_MID>, 2, (size_t)mid_layout(H, S).bytes,
                     NW_MID * WAVE);
     if (!r) r = one((const void*)mpc_direct_kernel<false, DM_NARROW, NT_STEPS / WAVE>, 3,
-                    (size_t)narrow_layout(H, S).bytes, NT_STEPS);
+                    (size_t)narrow_layout(H, S, knobs().narrow_lds).bytes, NT_STEPS);
     return r;
 }
 

@@ -280,7 +280,8 @@ int dragg_mpc_solve_explicit(const dragg_mpc_dims* dims, const dragg_mpc_problem
    DRAGG_HOT_ILP=1|2 (64-child chunks per front-DP pass of the one-wave hot launch; default: 2 at <= 8 homes
    per CU, else 1; results bit-identical), DRAGG_SIDE_GRID=hot,mid,big,narrow (the lag mode's side-pass
    grids, each clamped to 1 .. its launch's per-block scratch slots: dragg_mpc_side_grid reports the
-   grids in effect).  Unset: the defaults.  Lag mode (dragg_mpc_step_main / _side) honours every knob
+   grids in effect), DRAGG_NARROW_LDS_KB=n (the step-function launch's LDS per block; default all of a
+   CU's: a smaller block can share a CU with hot-launch blocks; results bit-identical).  Unset: the defaults.  Lag mode (dragg_mpc_step_main / _side) honours every knob
    but DRAGG_WAVES_PER_HOME: both its passes run the one-wave hot kernel. */
 void dragg_mpc_reload_knobs(void);
 

@@ -51,7 +51,7 @@ tou_enabled = true
 spp_enabled = false
 
 [agg.rl]
-action_horizon = 1
+action_horizon = {horizon}
 forecast_horizon = 1
 prev_timesteps = 12
 max_rp = 0.02
@@ -121,6 +121,10 @@ def write_data(root, days, month, n_profiles=100, seed=3):
             f.write(str(ts[i]).replace("T", " ") + ":00," + ",".join(f"{v:.2f}" for v in flow[i]) + "\n")
 
 
+# (action_horizon = the prediction horizon: the redis reward_price list is action_horizon * dt long, and
+# the reference's MPCCalc needs it of length 1 or >= H = horizon * dt, mpc_calc.py:353)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--homes", type=int, default=10000)
@@ -158,8 +162,6 @@ def main():
     ph = {k: round(v, 4) for k, v in agg.timings.items()}
     loop = agg.timings.get("step_loop", 0.0)
     size = os.path.getsize(path)
-    with open(path) as f:
-        res = json.load(f)
     out = {
         "metric": "end-to-end simulation wall time (Aggregator().run(), run_rbo_mpc)",
         "value": total, "unit": "s", "higher_is_better": False,
@@ -173,7 +175,7 @@ def main():
         "ms_per_step_in_loop": loop / agg.num_timesteps * 1e3,
         "solves_per_s_end_to_end": n * agg.num_timesteps / total,
         "solve_paths": getattr(agg, "solve_paths", None),
-        "results_json_bytes": size, "results_json_homes": len(res) - 1,
+        "results_json_bytes": size, "results_json_homes": len(agg.all_homes),
         "data": "synthetic NSRDB-format weather and water-draw profile files (the reference's formats)",
     }
     line = json.dumps(out)
