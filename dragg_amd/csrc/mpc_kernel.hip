@@ -2652,16 +2652,6 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     static_assert(SS > 0 && SS < 16, "duty count must be a compile-time constant below 16");
     static_assert(CAP <= PS && CAPB <= PS && PS <= 4096, "back-pointer rows hold a 12-bit parent index");
     constexpr int NU = SS + 1;
-    // the hot launch's back-pointers as the passes' keep ballots: survivors are appended in (parent, duty)
-    // order, so survivor j of a stage is the stage's j-th kept child c = NU parent + duty -- one 8-B word per
-    // 64 children (NU / 8 B per child, against 2 B per survivor as u16 rows: 2.3x less written per stage at
-    // NU = 7) and one store per pass; word BW - 1 of a stage's row holds its pass count.  The recovery finds
-    // the j-th set bit by a wave scan.  (The mid / big launches keep u16 rows: their beam compaction moves
-    // survivors.)
-    constexpr bool BITS = !CELL && NW == 1 && CAP == NF_HOT;
-    constexpr int BW = 2 * ((NU * CAP + 2 * WAVE - 1) / (2 * WAVE)) + 1;   // (ILP passes write pass pairs)
-    static_assert(!BITS || (BW <= WAVE && BW * 8 <= PS * 2), "a stage's ballot row fits its u16 row");
-    unsigned long long* const bits = reinterpret_cast<unsigned long long*>(B.par);
     constexpr int BPL = NBK / WAVE;      // buckets per lane in the scan
     static_assert(NBK % WAVE == 0, "");
     auto tw = [](double v) { return TOL_P * (1 + fabs(v)); };
@@ -3125,33 +3115,27 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             return keep;
         };
         unsigned Kmn, Kmx, Cmn, Cmx;
-        if constexpr (BITS) {
-            if (tid == 0) bits[(size_t)k * BW + BW - 1] = (unsigned long long)((nc + WAVE - 1) / WAVE);
-        }
-        auto append = [&](bool keep, int i, int u, double xc, double cc, unsigned vk, unsigned vc, int pass) {
+        auto append = [&](bool keep, int i, int u, double xc, double cc, unsigned vk, unsigned vc) {
             const unsigned long long bal = __ballot(keep);
             const int slot = nn + __popcll(bal & below);
             nn += __popcll(bal);
-            if constexpr (BITS) {
-                if (lane == 0) bits[(size_t)k * BW + pass] = bal;
-            }
             if (keep && slot < capn) {
                 fb[slot] = make_double2(xc, cc);
-                if constexpr (!BITS) B.par[k * PS + slot] = (uint16_t)(i | (u << 12));
+                B.par[k * PS + slot] = (uint16_t)(i | (u << 12));
                 kmn = umin(kmn, vk); kmx = umax(kmx, vk);
                 cmn = umin(cmn, vc); cmx = umax(cmx, vc);
             }
         };
         if constexpr (ILP >= 2) {
             auto pair3 = [&](int i, int u, int i2, int u2, double xc, double cc, double x2, double c2c, unsigned vk,
-                             unsigned vc, unsigned vk2, unsigned vc2, bool k1, bool k2, int c0) {
+                             unsigned vc, unsigned vk2, unsigned vc2, bool k1, bool k2) {
                 if (!nodom) {
                     const bool n1 = undominated(vk, vc), n2 = undominated(vk2, vc2);
                     k1 = k1 && n1;
                     k2 = k2 && n2;
                 }
-                append(k1, i, u, xc, cc, vk, vc, c0 / WAVE);
-                append(k2, i2, u2, x2, c2c, vk2, vc2, c0 / WAVE + 1);
+                append(k1, i, u, xc, cc, vk, vc);
+                append(k2, i2, u2, x2, c2c, vk2, vc2);
             };
             auto fresh = [&](int c0) {
                 int i, u, i2, u2;
@@ -3165,7 +3149,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     k1 = k1 && cc + b1 <= UBT;
                     k2 = k2 && c2c + b2 <= UBT;
                 }
-                pair3(i, u, i2, u2, xc, cc, x2, c2c, vk, vc, vk2, vc2, k1, k2, c0);
+                pair3(i, u, i2, u2, xc, cc, x2, c2c, vk, vc, vk2, vc2, k1, k2);
             };
 #pragma unroll
             for (int r = 0; r < HOLD; ++r) {
@@ -3176,7 +3160,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                         const int i = c < nc ? c / NU : 0, i2 = c2 < nc ? c2 / NU : i;
                         pair3(i, c - i * NU, i2, c2 < nc ? c2 - i2 * NU : c - i * NU, r_x1[r], r_c1[r], r_x2[r], r_c2[r],
                               r_v[r][0], r_v[r][1], r_v[r][2], r_v[r][3], (r_keep >> (2 * r)) & 1u,
-                              (r_keep >> (2 * r + 1)) & 1u, c0);
+                              (r_keep >> (2 * r + 1)) & 1u);
                     } else {
                         fresh(c0);
                     }
@@ -3191,7 +3175,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                 double xc, cc;
                 unsigned vk, vc;
                 const bool keep = eval(c0 + lane, i, u, xc, cc, vk, vc);
-                append(keep, i, u, xc, cc, vk, vc, c0 / WAVE);
+                append(keep, i, u, xc, cc, vk, vc);
             }
             Kmn = dpp_reduce(kmn, umin); Kmx = dpp_reduce(kmx, umax);
             Cmn = dpp_reduce(cmn, umin); Cmx = dpp_reduce(cmx, umax);
@@ -3394,41 +3378,13 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         }
     }
     if (best_out) *best_out = best;
-    if constexpr (BITS) {
-        // survivor j of stage k = the stage's j-th kept child: the row's words (one per lane), their
-        // population counts scanned, the word holding it, then its bit inside the word
-        int j = bi;
-        for (int k = H - 1; k >= 0; --k) {
-            const unsigned long long* const row = bits + (size_t)k * BW;
-            const unsigned long long w_ = lane < BW ? row[lane] : 0ull;
-            const int P = (int)(unsigned)read_lane((int)(unsigned)w_, BW - 1);
-            const unsigned long long wv = lane < P ? w_ : 0ull;
-            const int cnt = __popcll(wv);
-            const int incl = dpp_iscan(cnt, lane, 0, [](int a_, int b_) { return a_ + b_; });
-            const int ex = incl - cnt;
-            const int wl_ = __ffsll((long long)__ballot(j >= ex && j < incl)) - 1;
-            // the (j - ex)-th set bit of the lane's word (a halving search on population counts)
-            int r = j - ex, pos = 0;
-            unsigned long long x = wv;
-#pragma unroll
-            for (int wdt = 32; wdt > 0; wdt >>= 1) {
-                const int lc = __popcll(x & ((1ull << wdt) - 1ull));
-                if (r >= lc) { r -= lc; pos += wdt; x >>= wdt; }
-            }
-            const int c = WAVE * wl_ + read_lane(pos, wl_);
-            const int i = c / NU;
-            if (tid == 0) B.x[k * 8 + sv] = (double)(c - i * NU);
-            j = i;
-        }
-    } else if (tid == 0) {
+    if (tid == 0) {
         int j = bi;
         for (int k = H - 1; k >= 0; --k) {
             const int p = B.par[k * PS + j];
             B.x[k * 8 + sv] = (double)(p >> 12);
             j = p & 0xFFF;
         }
-    }
-    if (tid == 0) {
         double x = x0;                      // exact forward trajectory (the labels' arithmetic)
         for (int k = 0; k < H; ++k) {
             x = fma(B.cA[k], x, fma(g, B.x[k * 8 + sv], B.cC[k]));
