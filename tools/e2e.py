@@ -136,28 +136,30 @@ def write_config(data, a, seed):
     return mix
 
 
-def completable_seed(data, outs, a, tries=16):
-    """The first random_seed from 12 on whose community the reference completes: a battery home whose t = 0
-    solve fails makes the reference raise KeyError at t = 1 (mpc_calc.py:280-289) -- the season draw keyed by
-    the seed decides it.  Each try runs the runner's own pipeline and t = 0 on the GPU (untimed)."""
-    import torch
-    from dragg_amd import _lib as L
+def completable_community(data, outs, a):
+    """The reference raises KeyError at t = 1 when a battery home's t = 0 solve fails (mpc_calc.py:280-289);
+    at 10k homes some battery home always does (the season draw keyed by the seed: 16 seeds tried in January
+    at H = 24, round 6).  So, untimed, as bench.py does: the runner's own pipeline and generator
+    (create_homes), then t = 0 on the GPU with the runner's environment and each failing battery home
+    swapped with a home without a battery (community.reference_completable), written as the run's
+    all_homes-N-config.json; the timed run loads it (overwrite_existing = false, aggregator.py:263-271).
+    -> (seconds of create_homes, battery-home swaps)"""
+    from dragg_amd import inputs as I
+    from dragg_amd import results as R
+    from dragg_amd.community import reference_completable
     from dragg_amd.runner import Aggregator
-    for seed in range(12, 12 + tries):
-        write_config(data, a, seed)
-        agg = Aggregator(data_dir=data, outputs_dir=outs)
-        agg.flush()
-        agg.get_homes()
-        agg.case = "e2e-probe"
-        dev = agg._device_community()
-        dev.run_iteration()
-        st = dev.status_hist[0].cpu().numpy()
-        bad = sum(1 for i, h in enumerate(dev.homes) if "battery" in h["type"] and st[i] != L.ST_OPTIMAL)
-        del dev, agg
-        torch.cuda.empty_cache()
-        if bad == 0:
-            return seed
-    raise SystemExit(f"no completable community among seeds 12..{12 + tries - 1}")
+    agg = Aggregator(data_dir=data, outputs_dir=outs)
+    agg.flush()
+    t0 = time.perf_counter()
+    agg.get_homes()
+    t_create = agg.timings.get("create_homes", time.perf_counter() - t0)
+    col = lambda c: agg.all_data[c].to_numpy(dtype=float)  # noqa: E731
+    homes, swaps = reference_completable(agg.all_homes, col("OAT"), col("GHI"), col("tou"),
+                                         int(agg.config["simulation"]["random_seed"]),
+                                         reward_price=list(agg.reward_price), start_index=agg.start_hour_index)
+    I.check_home_counts(homes, agg.config)
+    R.write_home_configs(outs, homes, len(homes))
+    return t_create, swaps
 
 
 def main():
@@ -171,8 +173,7 @@ def main():
     ap.add_argument("--workdir", default=None, help="data and outputs here (default: a temporary directory)")
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
-    ap.add_argument("--seed", type=int, default=None,
-                    help="simulation.random_seed (default: the first from 12 whose community the reference completes)")
+    ap.add_argument("--seed", type=int, default=12, help="simulation.random_seed")
     a = ap.parse_args()
     n = a.homes
     days = math.ceil((a.hours + a.horizon_hours + 2) / 24) + 1
@@ -184,9 +185,13 @@ def main():
     from dragg_amd.runner import Aggregator
     torch.cuda.init()
     torch.zeros(1, device="cuda")                 # (the CUDA context, outside the timed run)
-    seed = a.seed if a.seed is not None else completable_seed(data, os.path.join(work, "probe"), a)
+    seed = a.seed if a.seed is not None else 12
     mix = write_config(data, a, seed)
-    shutil.rmtree(os.path.join(work, "probe"), ignore_errors=True)
+    t_create, swaps = completable_community(data, outs, a)
+    with open(os.path.join(data, "config.toml")) as f:
+        txt = f.read().replace("overwrite_existing = true", "overwrite_existing = false")
+    with open(os.path.join(data, "config.toml"), "w") as f:
+        f.write(txt)
     t0 = time.perf_counter()
     agg = Aggregator(data_dir=data, outputs_dir=outs)
     path = agg.run()
@@ -201,6 +206,12 @@ def main():
         "config": {"homes": n, "steps": agg.num_timesteps, "H": a.horizon_hours * a.dt, "dt": a.dt,
                    "month": a.month, "checkpoint_interval": a.checkpoint, "homes_mix": mix, "random_seed": seed},
         "phases_s": ph,
+        "create_homes_generator_s": t_create,
+        "community": {"battery_home_swaps": swaps,
+                      "note": "the community create_homes draws (legacy-RNG order), with each battery home whose t = 0 "
+                              "solve fails swapped with a home without a battery (the reference raises KeyError at "
+                              "t = 1 otherwise), written as all_homes-N-config.json before the timed run, which "
+                              "loads it (phase create_homes); the generator itself took create_homes_generator_s"},
         "phase_note": "checkpoints = the in-loop check_errors + write_outputs + save_state (its results.json "
                       "write is also counted in history_gather / results_build / results_write); step_loop = the "
                       "steps' launches and device time without the checkpoint writes",

@@ -19,7 +19,7 @@ pass sq3 SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU
 pass sq4 SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT SQ_INST_CYCLES_SALU || exit 1
 pass fetch FETCH_SIZE || exit 1
 pass write WRITE_SIZE || exit 1
-if [ -f varlib/stats.so ]; then
-  DRAGG_LIB=varlib/stats.so timeout -k 10 200 python tools/front_stats.py 10000 12 7 --json $OUT/front_stats.json > $OUT/front_stats.log 2>&1 || exit 1
+if [ -f abl/stats.so ] && [ -z "$NO_STATS" ]; then
+  DRAGG_LIB=$PWD/abl/stats.so timeout -k 10 200 python tools/front_stats.py --json $OUT/front_stats.json -- $ARGS > $OUT/front_stats.log 2>&1 || exit 1
 fi
 echo done
