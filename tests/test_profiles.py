@@ -56,3 +56,38 @@ def test_bench_line_agrees_with_its_profile(rnd, name):
     assert r["traffic"] == pytest.approx(tj["bytes_per_step"] / (r["kernel_ms"] * 1e-3) / 1e9, rel=1e-9)
     if "dp_work" in line:
         assert line["dp_work"]["achieved"] == pytest.approx(tj["front_stats"]["children_per_step"] / ks / 1e9, rel=1e-9)
+
+
+def _lines(rnd):
+    d = os.path.join(ROOT, "profiles", rnd, "lines")
+    return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".json")) if os.path.isdir(d) else []
+
+
+@pytest.mark.parametrize("rnd", ["r06"])
+def test_every_line_cites_only_its_own_workloads_counters(rnd):
+    """a committed line takes its counters (roofline.traffic, the VALU / LDS
+    rooflines) only from a rocprofv3 pass of its own command -- the same workload, window, shard and steps
+    mode (bench.traffic_key since round 6) -- and has traffic null otherwise."""
+    lines = _lines(rnd)
+    if not lines:
+        pytest.skip("no committed lines of this round")
+    for path in lines:
+        line = json.load(open(path))
+        r = line.get("roofline") or {}
+        key = r.get("profile_key")
+        if line.get("metric", "").startswith("end-to-end"):
+            continue
+        assert key, path
+        shard = line.get("shard_emulation")
+        assert (", shard " in key) == bool(shard), (path, key)
+        if shard:
+            rank = "max" if shard.get("max_over_shards") else shard["shard_rank"]
+            assert f", shard {rank} of {shard['shard_of']}" in key, (path, key)
+        assert key.endswith(f", {line['steps_mode']} steps"), (path, key)
+        src = r.get("traffic_source")
+        if src is None:
+            assert r.get("traffic") is None and "roofline_valu" not in line, path
+            continue
+        tj = json.load(open(os.path.join(ROOT, src)))
+        assert tj["workload"] == key, (path, src)
+        assert os.path.dirname(src).endswith(rnd), (path, src)            # this round's build

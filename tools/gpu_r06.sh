@@ -55,8 +55,9 @@ run() { name=$1
 import json; d=json.load(open('$OUT/$name.json')); print('$name', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],4), 'ms/step', 'kern', round(d['roofline']['kernel_ms'],4), (d.get('shard_emulation') or {}).get('max_over_shards'), {k: v for k, v in d['status_counts'].items() if v and k != 'optimal'})"; }
 for spec in ${LINES:-full96}; do [ "$spec" = none ] || run $spec; done
 for E in $E2E; do
-  case $E in h24) hh=6; mo=1 ;; h48) hh=12; mo=7 ;; h24jul) hh=6; mo=7 ;; esac
-  timeout -k 10 ${E2E_LIMIT:-600} python3 -u tools/e2e.py --homes ${E2E_HOMES:-10000} --horizon-hours $hh --month $mo --out $OUT/e2e_$E.json > $OUT/e2e_$E.log 2>&1 || { echo "e2e $E failed"; tail -5 $OUT/e2e_$E.log; exit 1; }
+  ref=""
+  case $E in h24) hh=6; mo=1 ;; h48) hh=12; mo=7 ;; h24ref) hh=6; mo=1; ref=--reference-writer ;; h48ref) hh=12; mo=7; ref=--reference-writer ;; esac
+  timeout -k 10 ${E2E_LIMIT:-600} python3 -u tools/e2e.py --homes ${E2E_HOMES:-10000} --horizon-hours $hh --month $mo $ref --out $OUT/e2e_$E.json > $OUT/e2e_$E.log 2>&1 || { echo "e2e $E failed"; tail -5 $OUT/e2e_$E.log; exit 1; }
   python3 -c "import json; d=json.load(open('$OUT/e2e_$E.json')); print('e2e $E', round(d['value'],3), 's', {k: round(v,3) for k, v in d['phases_s'].items()})"
 done
 for TR in $TRACE; do
