@@ -76,10 +76,11 @@ constexpr int RS_HOLD = 4;               // ILP = 2 front DP: child pairs held i
 // exact pass's fronts then hold 22-280 labels, where the LP bound and the bucketed schedule's cost left
 // 30 % of the chains past 2,048)
 constexpr int NCELL = 1024;              // cells of the grid
-// a row of the cell bound in the workspace: NCELL 16-bit codes and its (offset, scale) as two f32; code q is the
-// lower bound offset + q scale (rounded DOWN at encoding, so it stays below the f32 row it stands for),
-// 0xFFFF is +inf.  Half the bytes of f32 rows (2 GB per launch at 10k homes, H = 48, round 5)
-constexpr int CELL_STRIDE = NCELL + 4;
+// a row of the cell bound in the workspace: NCELL 16-bit codes; code q is the lower bound offset + q scale with
+// one (offset, scale) per home (from the chain's duty costs: every cost-to-go lies in [sum of the negative,
+// sum of the positive stage costs]), rounded DOWN at encoding so that it stays below the f32 value it stands
+// for; 0xFFFF is +inf.  Half the bytes of f32 rows (2 GB per launch at 10k homes, H = 48, round 5)
+constexpr int CELL_STRIDE = NCELL;
 constexpr unsigned CELL_INF = 0xFFFFu;
 constexpr int BEAM_K = 32;               // labels a beam stage keeps (7 BEAM_K children fit NF_MID; measured
                                          //   RL action at 48: 20.1 ms, 32: 19.6 ms)
@@ -1544,7 +1545,8 @@ __host__ __device__ inline size_t w_region_bytes(int N, int H) { return (size_t)
 // the lag mode's side workspace: the lists and per-block scratch [defer_offset, w_region_offset)
 __host__ __device__ inline size_t side_workspace_bytes(int N, int H) { return w_region_offset(N, H) - defer_offset(N, H); }
 // then (256-aligned), with a reward-price list (dims.n_rp > 1: RL prices possible), the cell bound's
-// rows of every home's indoor-air chain [N][H + 1][CELL_STRIDE] u16 codes (cell_kernel; row 0: the valid flag)
+// rows of every home's indoor-air chain [N][H + 1][CELL_STRIDE] u16 codes (cell_kernel; row 0: the header --
+// valid flag, offset, scale as three f32)
 __host__ __device__ inline size_t cell_region_offset(int N, int H) {
     return (w_region_offset(N, H) + w_region_bytes(N, H) + 255) / 256 * 256;
 }
@@ -2393,6 +2395,7 @@ struct FrontBufs {
     // dp_front<..., CELL = true>: the cell bound in place of W
     const uint16_t* cg;                  // [H + 1][CELL_STRIDE] global: cell_rows' lower bounds of x_k's cost-to-go
     double c_lo, c_inv;                  // the grid: cell of x = floor((x - c_lo) c_inv)
+    float c_off, c_sc;                   // the codes' offset and scale (cell_rows)
 };
 
 // 1 / w to about 1 ulp: v_rcp_f64 and one Newton step (no IEEE division sequence)
@@ -2466,43 +2469,25 @@ DEV T dpp_iscan(T v, int lane, T id, Op op) {
 // x_{k+1}'s box (+inf where none) -- a minimum over a superset of the states a schedule can reach,
 // rounded down to f32.  r0 / r1: two LDS rows of scratch (NCELL + 1 floats each at least).  Every thread of the block calls it; false
 // (no bound) on a degenerate stage (A <= 0).
-// a cell's lower bound from a quantized row (offset + q scale, +inf for CELL_INF)
-DEV float cell_dec(const uint16_t* row, int c) {
-    const unsigned q = row[c];
-    const float* const hd = reinterpret_cast<const float*>(row + NCELL);
-    return q == CELL_INF ? INFINITY : fmaf((float)q, hd[1], hd[0]);
-}
-// row 0 of a home's cell rows holds no bound: its header's first float flags the rows valid (1)
-DEV bool cell_rows_valid(const uint16_t* cg) { return reinterpret_cast<const float*>(cg + NCELL)[0] == 1.0f; }
-// a row of NT threads' f32 values (LDS) to its 16-bit codes: offset = the least finite value, scale = the
-// finite range / 65534 rounded up; each code rounded down until its decoded value is at most the value
+// a cell's lower bound from its 16-bit code (offset + q scale, +inf for CELL_INF)
+DEV float cell_dec(unsigned q, float off, float sc) { return q == CELL_INF ? INFINITY : fmaf((float)q, sc, off); }
+// row 0 of a home's cell rows holds no bound: its first three f32 are the rows' valid flag (1), offset, scale
+DEV bool cell_rows_valid(const uint16_t* cg) { return reinterpret_cast<const float*>(cg)[0] == 1.0f; }
+DEV float cell_off(const uint16_t* cg) { return reinterpret_cast<const float*>(cg)[1]; }
+DEV float cell_sc(const uint16_t* cg) { return reinterpret_cast<const float*>(cg)[2]; }
+// a row of f32 lower bounds (LDS) to its 16-bit codes: each code rounded down until its decoded value is at
+// most the value (one step at most but where the scale is below the value's ulp)
 template <int NT>
-DEV void cell_store(uint16_t* row, const float* v, int tid) {
-    __shared__ float red[2][NT / WAVE];
-    float lo = INFINITY, hi = -INFINITY;
-    for (int j = tid; j < NCELL; j += NT)
-        if (v[j] < INFINITY) { lo = fminf(lo, v[j]); hi = fmaxf(hi, v[j]); }
-    lo = dpp_reduce(lo, [](float a, float b) { return fminf(a, b); });
-    hi = dpp_reduce(hi, [](float a, float b) { return fmaxf(a, b); });
-    if ((tid & (WAVE - 1)) == 0) { red[0][tid / WAVE] = lo; red[1][tid / WAVE] = hi; }
-    __syncthreads();
-    lo = INFINITY; hi = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NT / WAVE; ++w) { lo = fminf(lo, red[0][w]); hi = fmaxf(hi, red[1][w]); }
-    const bool any = lo < INFINITY;
-    const float off = any ? lo : 0.0f;
-    const float sc = any && hi > lo ? __double2float_ru(((double)hi - (double)lo) / 65534.0) : 0.0f;
+DEV void cell_store(uint16_t* row, const float* v, int tid, float off, float sc, float inv) {
     for (int j = tid; j < NCELL; j += NT) {
         const float x = v[j];
         unsigned q = CELL_INF;
         if (x < INFINITY) {
-            q = sc > 0.0f ? (unsigned)fmin(65534.0, fmax(0.0, floor(((double)x - (double)off) / (double)sc))) : 0u;
+            q = (unsigned)fminf(65534.0f, fmaxf(0.0f, floorf((x - off) * inv)));
             while (q > 0 && fmaf((float)q, sc, off) > x) --q;
         }
         row[j] = (uint16_t)q;
     }
-    if (tid == 0) { reinterpret_cast<float*>(row + NCELL)[0] = off; reinterpret_cast<float*>(row + NCELL)[1] = sc; }
-    __syncthreads();                                     // (red is reused by the next row)
 }
 
 // the cell grid over a chain's box [bl, bh] (widened past every tolerance of the labels' box tests)
@@ -2522,6 +2507,18 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
     auto bxh = [&](int k) { const double b = k <= 1 ? hi0 : hi; return b + tw(b); };
     for (int k = 0; k < H; ++k)
         if (!(cA[k] > 0.0)) return false;                  // (uniform)
+    // the codes' scale: every cost-to-go of x_k (k >= 1) lies in [sum of min(0, q_j S), sum of max(0, q_j S)]
+    // over j >= 1 (the rows' values are rounded down below their true ones: the offset sits a margin lower)
+    double slo = 0.0, shi = 0.0;
+    for (int k = 1; k < H; ++k) { slo += fmin(0.0, cq[k] * S); shi += fmax(0.0, cq[k] * S); }
+    const float off = __double2float_rd(slo - 1e-6 * (1.0 + fabs(slo) + fabs(shi)));
+    const float sc = shi > (double)off ? __double2float_ru((shi - (double)off) / 65534.0) : 0.0f;
+    const float inv = sc > 0.0f ? 1.0f / sc : 0.0f;
+    if (tid == 0) {
+        float* const hd = reinterpret_cast<float*>(cg);      // row 0: the header (valid flag written by the caller)
+        hd[1] = off;
+        hd[2] = sc;
+    }
     // cells meeting a box [l, h]: [cell(l - eps), cell(h + eps)] (clamped to the grid)
     auto cell_span = [&](double l, double h, int& c0, int& c1) {
         c0 = max(0, (int)floor((l - eps - c_lo) * c_inv));
@@ -2533,7 +2530,7 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
         for (int j = tid; j < NCELL; j += NT) r0[j] = (j >= c0 && j <= c1) ? 0.0f : INFINITY;
     }
     __syncthreads();
-    cell_store<NT>(cg + (size_t)H * CELL_STRIDE, r0, tid);
+    cell_store<NT>(cg + (size_t)H * CELL_STRIDE, r0, tid, off, sc, inv);
     float* nxt = r0;
     float* cur = r1;
     for (int k = H - 1; k >= 1; --k) {
@@ -2588,7 +2585,7 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
                 if (j < NCELL) cur[j] = outv[r];
             }
             __syncthreads();
-            cell_store<NT>(cg + (size_t)k * CELL_STRIDE, cur, tid);
+            cell_store<NT>(cg + (size_t)k * CELL_STRIDE, cur, tid, off, sc, inv);
             float* t_ = nxt; nxt = cur; cur = t_;
             continue;
         }
@@ -2623,7 +2620,7 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
             cur[j] = best < INFINITY ? __double2float_rd(best) : INFINITY;
         }
         __syncthreads();
-        cell_store<NT>(cg + (size_t)k * CELL_STRIDE, cur, tid);
+        cell_store<NT>(cg + (size_t)k * CELL_STRIDE, cur, tid, off, sc, inv);
         float* t_ = nxt; nxt = cur; cur = t_;
     }
     return true;
@@ -2855,7 +2852,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     const uint16_t* crow = B.cg + CELL_STRIDE;
     auto cell_at = [&](double x) -> double {
         const int c = min(NCELL - 1, max(0, (int)floor((x - B.c_lo) * B.c_inv)));
-        return (double)cell_dec(crow, c);
+        return (double)cell_dec(crow[c], B.c_off, B.c_sc);
     };
     auto bound_at = [&](double x, int wst_) -> double {
         if constexpr (CELL) return cell_at(x); else return w_eval(B, x, wst_);
@@ -3415,7 +3412,7 @@ DEV bool round_duties(const Home& h, const Lds& L, int lane, uint16_t* par) {
     B.cA = cA; B.cC = cC; B.cq = cq; B.x = L.x; B.par = par;
     B.wg = nullptr; B.wlx = B.wlv = B.wls = nullptr;     // no bound pruning on this path
     B.xch = nullptr;                                     // one wave
-    B.cg = nullptr; B.c_lo = 0.0; B.c_inv = 0.0;
+    B.cg = nullptr; B.c_lo = 0.0; B.c_inv = 0.0; B.c_off = 0.0f; B.c_sc = 0.0f;
     const bool front = h.S == 6 && par != nullptr && (f - L.Lf) <= 128 * H;
     for (int k = lane; k < H; k += WAVE) {
         cA[k] = h.aT;
@@ -4571,13 +4568,14 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                 double c_lo = 0.0, c_inv = 0.0;
                 const bool have_cells = SECOND && rl_prices && h.S == 6 && chain == 0 && a.d.n_rp > 1 && cell_rows_valid(cg);
                 if (have_cells) cell_grid(fmin(lo0, lo), fmax(hi0, hi), c_lo, c_inv);
+                const float c_off = have_cells ? cell_off(cg) : 0.0f, c_sc = have_cells ? cell_sc(cg) : 0.0f;
                 const FrontBufs FB{reinterpret_cast<double2*>(sb + bl.fa), reinterpret_cast<double2*>(sb + bl.fb),
                                    reinterpret_cast<unsigned long long*>(sb + bl.kb),
                                    reinterpret_cast<unsigned long long*>(sb + bl.cb),
                                    reinterpret_cast<unsigned*>(sb + bl.mh), reinterpret_cast<unsigned*>(sb + bl.kl),
                                    reinterpret_cast<unsigned*>(sb + bl.flo), reinterpret_cast<unsigned*>(sb + bl.fhi),
                                    D.cA, D.cC, D.cq, D.x, bpar, wg, wl, wl + WAVE, wl + 2 * WAVE,
-                                   sb + bl.xch, cg, c_lo, c_inv};
+                                   sb + bl.xch, cg, c_lo, c_inv, c_off, c_sc};
                 // a chain the mid launch handed over: its upper-bound schedule (the beam's or the bucketed
                 // DP's) is in the solution rows already (the mid pass overflowed without writing them),
                 // only the big pass is left
@@ -4641,7 +4639,8 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                                     const double tl = lo0 - TOL_P * (1 + fabs(lo0)), th = hi0 + TOL_P * (1 + fabs(hi0));
                                     if (x1 >= tl && x1 <= th)
                                         v = fma(D.cq[0], (double)u,
-                                                (double)cell_dec(cg + CELL_STRIDE, min(NCELL - 1, max(0, (int)floor((x1 - c_lo) * c_inv)))));
+                                                (double)cell_dec(cg[CELL_STRIDE + min(NCELL - 1, max(0, (int)floor((x1 - c_lo) * c_inv)))],
+                                                                 c_off, c_sc));
                                 }
                                 lo_u = dpp_reduce(v, [](double a_, double b_) { return fmin(a_, b_); });
                             }
@@ -4821,7 +4820,7 @@ __global__ __launch_bounds__(NT_CELL, 4) void cell_kernel(KArgs a) {
                                               c_lo, c_inv, tid);
         pf.mark(DRAGG_PH_FACTOR);                  // (diagnostic: the cell rows, in the factor slot)
         if (tid == 0) {
-            reinterpret_cast<float*>(cg + NCELL)[0] = ok ? 1.0f : 0.0f;
+            reinterpret_cast<float*>(cg)[0] = ok ? 1.0f : 0.0f;
             if (pf.on) {
                 a.out.cycles[(size_t)DRAGG_PH_CHECK * N + home] = (int64_t)pf.acc[DRAGG_PH_CHECK];
                 a.out.cycles[(size_t)DRAGG_PH_FACTOR * N + home] = (int64_t)pf.acc[DRAGG_PH_FACTOR];
