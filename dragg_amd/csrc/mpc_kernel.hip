@@ -2475,19 +2475,13 @@ DEV float cell_dec(unsigned q, float off, float sc) { return q == CELL_INF ? INF
 DEV bool cell_rows_valid(const uint16_t* cg) { return reinterpret_cast<const float*>(cg)[0] == 1.0f; }
 DEV float cell_off(const uint16_t* cg) { return reinterpret_cast<const float*>(cg)[1]; }
 DEV float cell_sc(const uint16_t* cg) { return reinterpret_cast<const float*>(cg)[2]; }
-// a row of f32 lower bounds (LDS) to its 16-bit codes: each code rounded down until its decoded value is at
-// most the value (one step at most but where the scale is below the value's ulp)
-template <int NT>
-DEV void cell_store(uint16_t* row, const float* v, int tid, float off, float sc, float inv) {
-    for (int j = tid; j < NCELL; j += NT) {
-        const float x = v[j];
-        unsigned q = CELL_INF;
-        if (x < INFINITY) {
-            q = (unsigned)fminf(65534.0f, fmaxf(0.0f, floorf((x - off) * inv)));
-            while (q > 0 && fmaf((float)q, sc, off) > x) --q;
-        }
-        row[j] = (uint16_t)q;
-    }
+// a f32 lower bound to its 16-bit code, rounded down: decoded, it is at most x (the scale is at least 4 ulps of
+// every value of the chain's range, so one step down after the floor suffices; x >= the offset)
+DEV unsigned cell_enc(float x, float off, float sc, float inv) {
+    if (!(x < INFINITY)) return CELL_INF;
+    float qf = fminf(65534.0f, fmaxf(0.0f, floorf((x - off) * inv)));
+    if (fmaf(qf, sc, off) > x) qf -= 1.0f;
+    return (unsigned)fmaxf(qf, 0.0f);
 }
 
 // the cell grid over a chain's box [bl, bh] (widened past every tolerance of the labels' box tests)
@@ -2512,8 +2506,8 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
     double slo = 0.0, shi = 0.0;
     for (int k = 1; k < H; ++k) { slo += fmin(0.0, cq[k] * S); shi += fmax(0.0, cq[k] * S); }
     const float off = __double2float_rd(slo - 1e-6 * (1.0 + fabs(slo) + fabs(shi)));
-    const float sc = shi > (double)off ? __double2float_ru((shi - (double)off) / 65534.0) : 0.0f;
-    const float inv = sc > 0.0f ? 1.0f / sc : 0.0f;
+    const float sc = __double2float_ru(fmax((shi - (double)off) / 65534.0, (fabs((double)off) + fabs(shi) + 1e-30) * 0x1p-21));
+    const float inv = 1.0f / sc;
     if (tid == 0) {
         float* const hd = reinterpret_cast<float*>(cg);      // row 0: the header (valid flag written by the caller)
         hd[1] = off;
@@ -2527,10 +2521,13 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
     {
         int c0, c1;
         cell_span(bxl(H), bxh(H), c0, c1);
-        for (int j = tid; j < NCELL; j += NT) r0[j] = (j >= c0 && j <= c1) ? 0.0f : INFINITY;
+        for (int j = tid; j < NCELL; j += NT) {
+            const float v = (j >= c0 && j <= c1) ? 0.0f : INFINITY;
+            r0[j] = v;
+            cg[(size_t)H * CELL_STRIDE + j] = (uint16_t)cell_enc(v, off, sc, inv);
+        }
     }
     __syncthreads();
-    cell_store<NT>(cg + (size_t)H * CELL_STRIDE, r0, tid, off, sc, inv);
     float* nxt = r0;
     float* cur = r1;
     for (int k = H - 1; k >= 1; --k) {
@@ -2582,10 +2579,9 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
 #pragma unroll
             for (int r = 0; r < (NCELL + NT - 1) / NT; ++r) {
                 const int j = r * NT + tid;
-                if (j < NCELL) cur[j] = outv[r];
+                if (j < NCELL) { cur[j] = outv[r]; cg[(size_t)k * CELL_STRIDE + j] = (uint16_t)cell_enc(outv[r], off, sc, inv); }
             }
             __syncthreads();
-            cell_store<NT>(cg + (size_t)k * CELL_STRIDE, cur, tid, off, sc, inv);
             float* t_ = nxt; nxt = cur; cur = t_;
             continue;
         }
@@ -2617,10 +2613,11 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
                     if (m < INFINITY) best = fmin(best, fma(q, (double)u, (double)m));
                 }
             }
-            cur[j] = best < INFINITY ? __double2float_rd(best) : INFINITY;
+            const float v = best < INFINITY ? __double2float_rd(best) : INFINITY;
+            cur[j] = v;
+            cg[(size_t)k * CELL_STRIDE + j] = (uint16_t)cell_enc(v, off, sc, inv);
         }
         __syncthreads();
-        cell_store<NT>(cg + (size_t)k * CELL_STRIDE, cur, tid, off, sc, inv);
         float* t_ = nxt; nxt = cur; cur = t_;
     }
     return true;
