@@ -2387,7 +2387,7 @@ struct FrontBufs {
                                          //   over the chain's widened box, rounded outward
     const double *cA, *cC, *cq;          // [H] chain coefficients and duty costs
     double* x;                           // [8H] stage-slot solution (writes slots sx, sv)
-    uint16_t* par;                       // [H][NB_CAP] global
+    uint16_t* par;                       // global back-pointer rows, packed densely (row k at flo[k])
     double2* wg;                         // [H + 1][WAVE] global: LP cost-to-go W_j as points (x, v),
                                          //   +inf padded; nullptr = no bound pruning
     double *wlx, *wlv, *wls;             // [WAVE] LDS: the current stage's W (points, slopes)
@@ -2880,11 +2880,17 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
     unsigned long long sp_acc[7] = {0, 0, 0, 0, 0, 0, 0}, sp_t = __builtin_amdgcn_s_memtime();
 #define SP_MARK(i) do { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); sp_acc[i] += n_ - sp_t; sp_t = n_; } while (0)
 #endif
+    // back-pointer rows are packed densely: row k (the survivors of stage k) starts at pbase, kept in
+    // B.flo[k] (dead from stage k on: stage k - 1 was its last reader), so that a home's rows are
+    // one contiguous run of ~sum n_k entries (the traceback stages them in LDS, below)
+    int pbase = 0;
     for (int k = 0; k < H; ++k) {
 #ifdef DRAGG_STAGE_PROF
         sp_acc[5] += 1;
         sp_t = __builtin_amdgcn_s_memtime();
 #endif
+        if (tid == 0) B.flo[k] = (unsigned)pbase;
+        uint16_t* const prow = B.par + pbase;
         // a front past PRUNE_AT labels (a tariff boundary inside the horizon): build the LP
         // bound now and prune the remaining stages by it.  Only while the front fits the bounded
         // capacity (the W table's LDS follows it) -- and, when fa is that buffer, stays clear of it.
@@ -3115,7 +3121,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             nn += __popcll(bal);
             if (keep && slot < capn) {
                 fb[slot] = make_double2(xc, cc);
-                B.par[k * PS + slot] = (uint16_t)(i | (u << 12));
+                prow[slot] = (uint16_t)(i | (u << 12));
                 kmn = umin(kmn, vk); kmx = umax(kmx, vk);
                 cmn = umin(cmn, vc); cmx = umax(cmx, vc);
             }
@@ -3215,7 +3221,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     const int slot = off + __popcll(bal & below);
                     if (slot < capn) {
                         fb[slot] = make_double2(fma(A, Li.x, fma(g, (double)u, C)), fma(q, (double)u, Li.y));
-                        B.par[k * PS + slot] = (uint16_t)(i | (u << 12));
+                        prow[slot] = (uint16_t)(i | (u << 12));
                     }
                 }
                 off += __popcll(bal);
@@ -3295,7 +3301,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     bool must = false, cand = false;
                     if (i < nn) {
                         Li = fb[i];
-                        pr = B.par[k * PS + i];
+                        pr = prow[i];
                         const double f = f_of(i);
                         must = f < thr_in;
                         cand = !must && f < fcut;
@@ -3308,7 +3314,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
                     kept += __popcll(bal);
                     if (keep_ && pos_ < beam_k) {
                         fb[pos_] = Li;
-                        B.par[k * PS + pos_] = pr;
+                        prow[pos_] = pr;
                     }
                 }
                 nn = min(kept, beam_k);
@@ -3346,6 +3352,7 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
 #endif
         double2* tmp = fa; fa = fb; fb = tmp;
         n = nn;
+        pbase += nn;
     }
 #ifdef DRAGG_STAGE_PROF
     if (tid == 0) for (int i = 0; i < 7; ++i) B.x[i * 8 + S_PAD] += (double)sp_acc[i];
@@ -3372,16 +3379,35 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
         }
     }
     if (best_out) *best_out = best;
+    // the traceback: H dependent reads of the back-pointer rows.  When the dense rows (pbase entries)
+    // and the duties fit the fronts' LDS (dead now), one coalesced copy puts them there, so that those
+    // reads and the forward pass's are LDS round trips, not L2 ones (A/B: driver window -0.7 %, RL
+    // action -3 %)
+    double2* const f0 = fa < fb ? fa : fb;
+    const int cap_b = ((fa < fb ? fb : fa) == f0 + CAP ? 2 : 1) * CAP * (int)sizeof(double2);
+    const int tb = (2 * pbase + 15) / 16 * 16;
+    const bool staged = tb + H <= cap_b && (reinterpret_cast<uintptr_t>(B.par) & 15) == 0;
+    uint16_t* const lpar = reinterpret_cast<uint16_t*>(f0);
+    uint8_t* const ldu = reinterpret_cast<uint8_t*>(f0) + tb;
+    __syncthreads();
+    if (staged) {
+        const uint4* src = reinterpret_cast<const uint4*>(B.par);
+        uint4* dst = reinterpret_cast<uint4*>(f0);
+        for (int i = tid; i < tb / 16; i += NT) dst[i] = src[i];
+        __syncthreads();
+    }
     if (tid == 0) {
+        const uint16_t* const pr = staged ? lpar : B.par;
         int j = bi;
         for (int k = H - 1; k >= 0; --k) {
-            const int p = B.par[k * PS + j];
+            const int p = pr[B.flo[k] + j];
             B.x[k * 8 + sv] = (double)(p >> 12);
+            if (staged) ldu[k] = (uint8_t)(p >> 12);
             j = p & 0xFFF;
         }
         double x = x0;                      // exact forward trajectory (the labels' arithmetic)
         for (int k = 0; k < H; ++k) {
-            x = fma(B.cA[k], x, fma(g, B.x[k * 8 + sv], B.cC[k]));
+            x = fma(B.cA[k], x, fma(g, staged ? (double)ldu[k] : B.x[k * 8 + sv], B.cC[k]));
             B.x[k * 8 + sx] = x;
         }
     }
