@@ -15,6 +15,10 @@ if [ "$TESTS" != "none" ]; then
   timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest $TESTS -m gpu -x -v -s --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest.log; exit 1; }
   tail -2 $OUT/pytest.log
 fi
+if [ -n "$SMOKE" ]; then
+  timeout -k 10 300 python3 -u -c 'import __graft_entry__ as g; g.smoke()' > $OUT/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -20 $OUT/smoke.log; exit 1; }
+  tail -2 $OUT/smoke.log
+fi
 args_of() {
   case $1 in
     driver) echo --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 ;;
