@@ -258,6 +258,8 @@ class MPCBatch:
                 "lists": torch.zeros((ring, 2, L.lag_list_ints(self.N)), dtype=torch.int32, device=dev),
                 "clock": torch.zeros(max(1, self.N), dtype=torch.int32, device=dev),
                 "side_ws": self._side_workspace() if self.workspace is not None else None,
+                # (a high-priority side stream, measured in round 6: no change -- the 8-way shard holding
+                # home 7519 0.8476-0.8482 against 0.8457-0.8489 ms/step, profiles/r06/ab/prio*)
                 "stream": torch.cuda.Stream(device=dev),
                 "main_done": torch.cuda.Event(),
                 "side_done": [torch.cuda.Event() for _ in range(ring)],

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-6 A/B: the in-tree build (dense back-pointers + no zero stores of unread slots) against dense2 (dense
+# only) and base (before the dense rows): GPU tests on the in-tree build, then the driver window and the full
+# day of the 8-way shard holding home 7519 (tools/gpu_ab6.sh).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out/ab9
+timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab9/tests.log 2>&1 || { tail -30 gpurun_out/ab9/tests.log; exit 1; }
+tail -1 gpurun_out/ab9/tests.log
+TAG=ab9d ROUNDS=2 bash tools/gpu_ab6.sh "$@" || exit 1
+TAG=ab9s ROUNDS=2 ABARGS="--steps 96 --warmup 4 --shard-of 8 --shard-rank 7" bash tools/gpu_ab6.sh "$@" || exit 1
+echo ab9-done
