@@ -4383,8 +4383,12 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                     D.cA[k] = h.aT;
                     D.cC[k] = D.oat[k + 1] * h.iR * 3600 * h.inv_c;
                     D.cq[k] = wk * h.Pact;
-                    D.x[k * 8 + S_PAD] = 0.0;
-                    D.x[k * 8 + S_CH] = 0.0; D.x[k * 8 + S_DIS] = 0.0; D.x[k * 8 + S_E] = 0.0;
+#if defined(DRAGG_FRONT_STATS) || defined(DRAGG_FRONT_STATS2) || defined(DRAGG_STAGE_PROF) || defined(DRAGG_STEP_PROF)
+                    D.x[k * 8 + S_PAD] = 0.0;             // (the diagnostics' accumulators)
+#endif
+                    // the battery slots are read only for a battery home (objective, write_success), whose
+                    // battery LP writes them all: the other homes skip the stores (1.5 KB per home-step)
+                    if (h.batt) { D.x[k * 8 + S_CH] = 0.0; D.x[k * 8 + S_DIS] = 0.0; D.x[k * 8 + S_E] = 0.0; }
                 } else {
                     const double df = D.draw[k + 1] / h.V, rem = 1 - df, d15 = df * TAP;
                     D.cA[k] = rem + (-rem * h.iRw) * 3600 * h.inv_w;
