@@ -3238,9 +3238,10 @@ DEV int dp_front(const FrontBufs& B, int H, int tid, double g, double x0, double
             // only moves down), its back-pointer with it
             if (beam_k > 0 && nn > beam_k && nn <= capn) {
                 // each label's cost + bound once (its cell row is in the workspace) into the key buckets'
-                // LDS, free until the stage's end (beam fronts: nn <= 7 beam_k <= NBK doubles)
+                // LDS, free until the stage's end (beam fronts: nn <= 7 beam_k = 224 <= 2 NBK doubles in the mid
+                // launch; with NBK doubles only, as before round 6, the cache never held: RL action -1.4 %)
                 double* const fv = reinterpret_cast<double*>(B.kb);
-                const bool fcache = nn <= NBK;
+                const bool fcache = nn <= 2 * NBK;         // (the key buckets' 16-B records: 2 NBK doubles)
                 double fl = INFINITY, fh = -INFINITY;
                 for (int i = lane; i < nn; i += WAVE) {
                     const double2 Li = fb[i];
