@@ -93,6 +93,11 @@ class DeviceAggregator:
             self._flag_host = torch.zeros(K, dtype=torch.int32, pin_memory=pin)
             self._flag_ev = [torch.cuda.Event() if pin else None for _ in range(K)]
             self._flag_step = [-1] * K
+            # the flag of a step is reduced and copied on a stream of its own, from the step's path_hist row
+            # (written once): the main stream's steps go on with no reduction kernels or device-to-host copy
+            # between them (on the main stream those cost +3.8 % per step against serial steps, round 6)
+            self._flag_stream = torch.cuda.Stream(device=dev) if pin else None
+            self._flag_src = [torch.cuda.Event() if pin else None for _ in range(K)]
             self.lag_from = None             # the first step run in lag mode
 
     FLAG_LAG = 2                 # adaptive start: steps the host may run ahead of the last flag it reads
@@ -114,12 +119,20 @@ class DeviceAggregator:
         return self._lagging
 
     def _flag(self, t):
-        """After a serial step t: did it hand a chain to the step-function DP?  (device -> pinned host, async)"""
+        """After a serial step t: did it hand a chain to the step-function DP?  (device -> pinned host, async,
+        on the flag stream after the step's path_hist row is written)"""
         K = len(self._flag_step)
-        f = ((self.batch.int_path & L.PATH_STEPS) != 0).any().to(torch.int32)
-        self._flag_host[t % K:t % K + 1].copy_(f.reshape(1), non_blocking=True)
-        if self._flag_ev[t % K] is not None:
-            self._flag_ev[t % K].record()
+        if self._flag_stream is None:
+            f = ((self.path_hist[t] & L.PATH_STEPS) != 0).any().to(torch.int32)
+            self._flag_host[t % K:t % K + 1].copy_(f.reshape(1))
+        else:
+            src = self._flag_src[t % K]
+            src.record()                                   # the main stream, after the path_hist[t] copy
+            with torch.cuda.stream(self._flag_stream):
+                self._flag_stream.wait_event(src)
+                f = ((self.path_hist[t] & L.PATH_STEPS) != 0).any().to(torch.int32)
+                self._flag_host[t % K:t % K + 1].copy_(f.reshape(1), non_blocking=True)
+                self._flag_ev[t % K].record(self._flag_stream)
         self._flag_step[t % K] = t
 
     # aggregator.py:711-726
