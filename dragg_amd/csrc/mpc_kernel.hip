@@ -4557,7 +4557,9 @@ DEV void solve_direct(const KArgs& a, int home, double* smem, int slot, int firs
                     r = dp_front<6, NF_HOT, NF_HOT, NB_CAP, NTB_HOT, NW, false, ILP>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv,
                                                                                    use_bound);
                 else
-                    r = dp_front<6, NF, NF_BOUND, NB_CAP, NTB, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
+                    // (64 key / cost buckets, as in the hot launch: the RL tank chain's DP here, rotated A/B
+                    // round 6: RL action -2.0 % against 192 buckets, 128: -0.6 %; the full day unchanged)
+                    r = dp_front<6, NF, NF_BOUND, NB_CAP, NTB_HOT, NW>(FB, H, lane, g, x0, lo0, hi0, lo, hi, sx, sv, use_bound);
 #ifdef DRAGG_FRONT_STATS2
                 // diagnostic: the T chain's fronts when the bound is the optimum itself
                 if (c0 && r == 1 && use_bound) {
