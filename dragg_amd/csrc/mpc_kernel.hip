@@ -2548,11 +2548,14 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
         if (Af + wdf < 1.0f) {
             // an image narrower than a cell meets cells i0 and i0 + 1 at most: the pair minima of V_{k+1}
             // once (pm[i + 1] = min(V[i], V[i + 1]), V = +inf past the grid), then one load per duty
-            float* const pm = cur;                 // (the stage's output row is written after: pm first)
+            // (with +inf pads: pp[i0 + 2] for a clamped i0 in [-2, NCELL + 1] is +inf at i0 = -2, NCELL, NCELL + 1
+            // and min(V[i0], V[i0 + 1]) between -- no range test per duty lookup: RL action -1.9 %, round 6)
+            float* const pp = cur;                 // (the stage's output row is written after: pp first)
             for (int i = tid; i <= NCELL; i += NT) {
                 const float va = i >= 1 ? nxt[i - 1] : INFINITY, vb = i < NCELL ? nxt[i] : INFINITY;
-                pm[i] = fminf(va, vb);
+                pp[i + 1] = fminf(va, vb);
             }
+            if (tid < 3) pp[tid == 0 ? 0 : NCELL + 1 + tid] = INFINITY;
             __syncthreads();
             float outv[(NCELL + NT - 1) / NT];
 #pragma unroll
@@ -2566,7 +2569,7 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
                     for (int u = 0; u <= SS; ++u) {
                         const float l = fmaf((float)u, guf, lj);
                         const int i0 = (int)floorf(fminf(fmaxf(l, -2.0f), (float)NCELL + 1.0f));
-                        mv[u] = (i0 >= -1 && i0 < NCELL) ? pm[i0 + 1] : INFINITY;
+                        mv[u] = pp[i0 + 2];
                     }
                     // f32: q rounded down (u >= 0), each sum lowered by 2 ulps past its rounding
 #pragma unroll
@@ -2575,7 +2578,7 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
                 }
                 outv[r] = best;
             }
-            __syncthreads();                       // (every thread read pm: the row may be written)
+            __syncthreads();                       // (every thread read pp: the row may be written)
 #pragma unroll
             for (int r = 0; r < (NCELL + NT - 1) / NT; ++r) {
                 const int j = r * NT + tid;
