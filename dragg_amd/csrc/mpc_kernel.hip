@@ -2470,6 +2470,9 @@ DEV T dpp_iscan(T v, int lane, T id, Op op) {
 // rounded down to f32.  r0 / r1: two LDS rows of scratch (NCELL + 1 floats each at least).  Every thread of the block calls it; false
 // (no bound) on a degenerate stage (A <= 0).
 // a cell's lower bound from its 16-bit code (offset + q scale, +inf for CELL_INF)
+// floor and convert in one instruction (v_cvt_flr_i32_f32; the compiler emits v_floor + v_cvt for (int)floorf):
+// the cell kernel's image indices, RL action -1.0 % (round 6)
+DEV int cvt_flr(float x) { int r; asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x)); return r; }
 DEV float cell_dec(unsigned q, float off, float sc) { return q == CELL_INF ? INFINITY : fmaf((float)q, sc, off); }
 // row 0 of a home's cell rows holds no bound: its first three f32 are the rows' valid flag (1), offset, scale
 DEV bool cell_rows_valid(const uint16_t* cg) { return reinterpret_cast<const float*>(cg)[0] == 1.0f; }
@@ -2568,7 +2571,7 @@ DEV bool cell_rows(uint16_t* cg, float* r0, float* r1, const double* cA, const d
 #pragma unroll
                     for (int u = 0; u <= SS; ++u) {
                         const float l = fmaf((float)u, guf, lj);
-                        const int i0 = (int)floorf(fminf(fmaxf(l, -2.0f), (float)NCELL + 1.0f));
+                        const int i0 = cvt_flr(fminf(fmaxf(l, -2.0f), (float)NCELL + 1.0f));
                         mv[u] = pp[i0 + 2];
                     }
                     // f32: q rounded down (u >= 0), each sum lowered by 2 ulps past its rounding
