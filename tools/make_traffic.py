@@ -15,6 +15,7 @@ steps + the committed step).  Per step (per action for RL):
 bench.py uses the file only when its key names the same workload and timed window."""
 import argparse
 import csv
+import gzip
 import re
 import json
 import os
@@ -50,11 +51,18 @@ def step_groups(rows, n_units, per_unit):
     return [sum(groups[u * per_unit:(u + 1) * per_unit], []) for u in range(n_units)]
 
 
+def _open(path):
+    """A raw pass CSV, or its gzipped copy (the committed raw passes of older rounds are gzipped)."""
+    if not os.path.exists(path) and os.path.exists(path + ".gz"):
+        return gzip.open(path + ".gz", "rt")
+    return open(path)
+
+
 def trace_ms(path, n_units, per_unit):
     """(mean, per-unit) kernel ms of the launches on the hot launch's stream, and the mean per unit of
     those on other streams (lag mode's side pass: it runs beside the main pass, so it is reported apart
     and not added; bench.py's HIP events time the main stream)"""
-    rows = list(csv.DictReader(open(path)))
+    rows = list(csv.DictReader(_open(path)))
     hot_streams = {r.get("Stream_Id") for r in rows if _hot(r["Kernel_Name"])}
     main, side = [], []
     for r in rows:
@@ -71,7 +79,7 @@ def trace_ms(path, n_units, per_unit):
 def counters(path, n_units, per_unit):
     """{counter: mean per unit} over the last n_units units of a PMC pass."""
     by = {}
-    for r in csv.DictReader(open(path)):
+    for r in csv.DictReader(_open(path)):
         by.setdefault(r["Counter_Name"], []).append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
     out = {}
     for c, rows in by.items():
@@ -126,7 +134,7 @@ def main():
     sq = {}
     for p in ("sq1", "sq2", "sq3", "sq4"):
         fp = os.path.join(a.prof, p, f"{p}_counter_collection.csv")
-        if os.path.exists(fp):
+        if os.path.exists(fp) or os.path.exists(fp + ".gz"):
             sq.update(counters(fp, a.steps, per_unit))
     if sq:
         out["sq_per_step"] = sq
